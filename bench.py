@@ -1,0 +1,204 @@
+"""Headline benchmark: Msamples/s (pixels x spp / s) rendering the RTIOW final scene at
+1920x1080, 1024 spp, max depth 10 (BASELINE.json metric, configs[3]) on N MI355X GPUs.
+
+One step = one DrawNextFrame of the whole frame: on every rank the gfx950 tracer renders the
+rank's interleaved 16-row stripes, then (N > 1) the stripes are all-gathered over RCCL and rank 0
+reassembles the frame. The frame is fixed as N grows (strong scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector, MI355X_MICROARCH.md chip table
+FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
+PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=1024)
+    p.add_argument("--depth", type=int, default=10)
+    p.add_argument("--scene", default="final")
+    p.add_argument("--variant", type=int, default=0)
+    p.add_argument("--blocks-per-cu", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
+                   help="target CPU work for the cpu_baseline sample")
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """The CPU oracle (C restatement of shader.comp) on a bounded sample of the same workload:
+    full-width rows y = 0, k, 2k, ... at the first s samples, on the host's cores."""
+    from tests import oracle_py
+    o = oracle_py.load()
+    threads = min(16, os.cpu_count() or 1)
+    scene = o.scene(args.scene)
+    # calibrate on a tiny sample, then size the real one for ~cpu_seconds of work
+    probe_rows, probe_spp = range(0, args.height, max(1, args.height // 8)), 2
+    t0 = time.perf_counter()
+    o.render(o.config(args.width, args.height, probe_spp, args.depth), scene, rows=probe_rows,
+             threads=threads)
+    dt = max(time.perf_counter() - t0, 1e-3)
+    rate = len(probe_rows) * args.width * probe_spp / dt  # samples/s
+    target = rate * args.cpu_seconds
+    spp = max(1, min(args.spp, 16))
+    nrows = max(1, min(args.height, int(target / (args.width * spp))))
+    step = max(1, args.height // nrows)
+    rows = range(0, args.height, step)
+    t0 = time.perf_counter()
+    o.render(o.config(args.width, args.height, spp, args.depth), scene, rows=rows, threads=threads)
+    dt = time.perf_counter() - t0
+    samples = len(rows) * args.width * spp
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/vcrt_oracle.c -O3, {threads} threads: rows y%{step}==0 "
+                      f"({len(rows)} rows x {args.width}) at spp {spp} of the same "
+                      f"{args.scene} scene/camera/depth {args.depth}; {samples} samples "
+                      f"in {dt:.2f} s",
+            "seconds": round(dt, 3)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import vulkancomputeraytracing_amd as vc
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
+                         max_depth=args.depth, device=local_rank, rank=rank, world_size=world,
+                         stripe_height=16, kernel_variant=args.variant,
+                         blocks_per_cu=args.blocks_per_cu)
+    rows_per_rank = max(len(vc.rows_for_rank(args.height, 16, world, r)) for r in range(world))
+    dev = torch.device("cuda", local_rank)
+    local = torch.zeros((rows_per_rank, args.width, 4), dtype=torch.float32, device=dev)
+    gathered = frame = None
+    if world > 1:
+        gathered = torch.empty((world, rows_per_rank, args.width, 4), dtype=torch.float32,
+                               device=dev)
+        if rank == 0:
+            frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
+
+    r = vc.Renderer(desc, args.scene)
+    r.set_framebuffer_device(local.data_ptr(), local.numel() * 4)
+    nspheres = len(vc.builtin_scene(args.scene))
+
+    def step():
+        r.draw_next_frame()  # returns when the rank's stripes are complete
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, local)
+            if rank == 0:
+                torch.cuda.current_stream().synchronize()
+                r.assemble_stripes(gathered.data_ptr(), frame.data_ptr(), rows_per_rank)
+
+    for i in range(args.warmup):
+        step()
+        log(f"[rank {rank}] warmup {i}: frame {r.stats()['frame_ms']:.1f} ms")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    kernel_ms, segments = [], []
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+        st = r.stats()
+        kernel_ms.append(st["kernel_ms"])
+        segments.append(st["segments"])
+        log(f"[rank {rank}] step {i}: frame {st['frame_ms']:.1f} ms, kernel "
+            f"{st['kernel_ms']:.1f} ms, {st['segments']} segments")
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = r.stats()
+    r.close()
+
+    if rank == 0:
+        samples = args.width * args.height * args.spp * args.steps
+        value = samples / elapsed / 1e6
+        k_ms = sum(kernel_ms) / len(kernel_ms)
+        seg = sum(segments) / len(segments)
+        flops = seg * nspheres * FLOPS_PER_SPHERE_TEST
+        achieved = flops / (k_ms * 1e-3) / 1e12
+        traffic = None
+        if os.path.exists(PROFILE_TRAFFIC):
+            try:
+                tr = json.load(open(PROFILE_TRAFFIC))
+                key = f"{args.scene}_{args.width}x{args.height}_s{args.spp}_d{args.depth}_n{world}"
+                traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        out = {
+            "metric": "Msamples/sec (pixels×spp/s) at 1920×1080, 1024spp, "
+                      "RTIOW final scene",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic RTIOW scene from SceneGenerator seed 5489)",
+            "config": {"workload": f"rtiow_{args.scene}_{args.width}x{args.height}_"
+                                   f"{args.spp}spp_d{args.depth}",
+                       "scene": args.scene, "spheres": nspheres, "width": args.width,
+                       "height": args.height, "spp": args.spp, "max_depth": args.depth,
+                       "parallelism": f"stripes16x{world}",
+                       "kernel_variant": st["kernel_variant"],
+                       "grid_blocks": st["grid_blocks"]},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3),
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
+                         "kernel": "vcrt_trace_lds" if st["kernel_variant"] == 1
+                         else "vcrt_trace_smem",
+                         "kernel_ms": round(k_ms, 3), "segments_per_launch": int(seg),
+                         "flops_per_launch": flops},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args)
+            except Exception as e:  # reported, never fatal to the GPU number
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+/* vcrt.h -- C ABI of the MI355X path tracer (libvcrt.so).
+ *
+ * This is the drop-in boundary. The reference renders from compile-time constants inside one
+ * Vulkan compute dispatch; this ABI carries the same state at run time and replaces:
+ *
+ *   vcrt_begin            <- VkResult BeginRenderingOperation(void)      include/Renderer.hpp:14
+ *                            (storage image Renderer.cpp:433-468, compute pipeline :532-543)
+ *   vcrt_draw_next_frame  <- VkResult DrawNextFrame(void)                include/Renderer.hpp:17
+ *                            (vkCmdDispatch(W/16,H/16,1) Renderer.cpp:221 + submit :678-686)
+ *   vcrt_end              <- VkResult EndRenderingOperation(void)        include/Renderer.hpp:20
+ *                            (idempotent teardown, tolerates partial Begin: Renderer.cpp:714-774)
+ *   vcrt_shader_load      <- VkResult CreateShaderStageFromFile(...)     include/Shader.hpp:14-15
+ *                            (loads the gfx950 code object instead of SPIR-V, Shader.cpp:34-95)
+ *   vcrt_set_scene        <- const sphere world[]                        globals.glsl:29-518
+ *   vcrt_scene_builtin /
+ *   vcrt_scene_generator_text <- SceneGenerator executable stdout        SceneGenerator.cpp:23-56
+ *   vcrt_render_desc      <- IMAGE_WIDTH/HEIGHT, SAMPLES_PER_PIXEL, MAX_RECURSION_LEVEL, camera
+ *                            globals.glsl:9-24, include/Common.hpp:23-24
+ *
+ * Added (the reference has no equivalents): read-back of the rgba32f framebuffer, statistics,
+ * rank/world stripe sharding and the stripe re-assembly used after a multi-GPU gather.
+ *
+ * Conventions: plain C types and pointers only. Every function returns a VkResult-compatible
+ * int32_t (0 = success, negative = error; values from the Vulkan registry). Nothing throws
+ * across the ABI. One renderer per process, calls are not reentrant (as in the reference).
+ */
+#ifndef VCRT_H
+#define VCRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t vcrt_result;
+
+/* VkResult values (Vulkan registry), defined locally: there are no Vulkan headers here. */
+#define VCRT_SUCCESS 0
+#define VCRT_NOT_READY 1
+#define VCRT_ERROR_OUT_OF_HOST_MEMORY (-1)
+#define VCRT_ERROR_OUT_OF_DEVICE_MEMORY (-2)
+#define VCRT_ERROR_INITIALIZATION_FAILED (-3)
+#define VCRT_ERROR_DEVICE_LOST (-4)
+#define VCRT_ERROR_FEATURE_NOT_PRESENT (-8)
+#define VCRT_ERROR_FORMAT_NOT_SUPPORTED (-11)
+#define VCRT_ERROR_UNKNOWN (-13)
+#define VCRT_ERROR_INCOMPATIBLE_SHADER_BINARY (1000482000) /* VK_..._SHADER_BINARY_EXT */
+
+/* Material ids, textures.glsl:10-12 */
+#define VCRT_TEXTURE_LAMBERTIAN 1
+#define VCRT_TEXTURE_METAL 2
+#define VCRT_TEXTURE_GLASS 3
+
+/* Same field order and size (40 B) as GLSL `struct sphere`, structures.glsl:10-16. */
+typedef struct vcrt_sphere {
+    float center[3];
+    float radius;
+    float colour[3];
+    float texture[3]; /* x = material id (as float), y = param (ratio / fuzz / eta), z unused */
+} vcrt_sphere;
+
+typedef struct vcrt_camera { /* globals.glsl:21-24 */
+    float lookfrom[3];
+    float lookat[3];
+    float vup[3];
+    float vfov; /* degrees */
+} vcrt_camera;
+
+/* Kernel variants. AUTO picks LDS staging when the sphere list fits, scalar cache otherwise. */
+#define VCRT_KERNEL_AUTO 0
+#define VCRT_KERNEL_LDS 1
+#define VCRT_KERNEL_SMEM 2
+
+typedef struct vcrt_render_desc {
+    uint32_t struct_size;      /* sizeof(vcrt_render_desc) */
+    int32_t width, height;     /* IMAGE_WIDTH, IMAGE_HEIGHT */
+    int32_t samples_per_pixel; /* SAMPLES_PER_PIXEL, >= 1 */
+    int32_t max_depth;         /* MAX_RECURSION_LEVEL, >= 0 */
+    vcrt_camera camera;
+    int32_t device;        /* HIP device ordinal; -1 = current device */
+    int32_t rank;          /* this process's shard of the frame */
+    int32_t world_size;    /* number of shards (GPUs) */
+    int32_t stripe_height; /* rows per interleaved stripe; 0 = 16 */
+    int32_t kernel_variant;
+    int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
+    const char* code_object_path; /* NULL = vcrt_tracer.hsaco next to libvcrt.so, then embedded */
+} vcrt_render_desc;
+
+typedef struct vcrt_stats {
+    uint64_t segments;     /* ray segments traced last frame (one full sphere-list scan each) */
+    uint64_t sphere_tests; /* segments * nspheres */
+    uint64_t samples;      /* local_rows * width * spp */
+    double kernel_ms;      /* tracer kernel time, HIP events on the render stream */
+    double frame_ms;       /* host wall time of the last vcrt_draw_next_frame */
+    int32_t frames;        /* frames drawn since vcrt_begin */
+    int32_t grid_blocks, block_threads, kernel_variant;
+    int32_t local_rows;    /* rows of this rank's packed framebuffer */
+    int32_t nspheres;
+    uint32_t lds_bytes;
+} vcrt_stats;
+
+/* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
+ * (13,2,3)->(0,0,0), vup (0,1,0), vfov 20, rank 0 of 1, stripe 16 (globals.glsl:9-24). */
+vcrt_result vcrt_default_desc(vcrt_render_desc* desc);
+
+vcrt_result vcrt_begin(const vcrt_render_desc* desc);
+vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count);
+vcrt_result vcrt_draw_next_frame(void);
+vcrt_result vcrt_end(void);
+
+/* Rows held by this rank: the rows y with (y / stripe_height) % world_size == rank, in order. */
+vcrt_result vcrt_local_rows(int32_t* rows);
+/* Copies the rank-local packed framebuffer (local_rows * width * 4 floats, rgba32f, row-major,
+ * top row first) to host memory. count = number of floats available at rgba. */
+vcrt_result vcrt_read_framebuffer(float* rgba, size_t count);
+/* Device address and size of the rank-local framebuffer (for collectives). */
+vcrt_result vcrt_framebuffer_device(void** device_ptr, size_t* bytes);
+/* Render into caller-owned device memory (>= local_rows*width*16 bytes); NULL = own buffer. */
+vcrt_result vcrt_set_framebuffer_device(void* device_ptr, size_t bytes);
+/* Rebuild a full frame from gathered rank framebuffers: gathered = [world][rows_per_rank][width]
+ * float4, frame = [height][width] float4, both device pointers. Runs on the render stream and
+ * returns when done. */
+vcrt_result vcrt_assemble_stripes(const void* gathered, void* frame, int32_t width,
+                                  int32_t height, int32_t world_size, int32_t stripe_height,
+                                  int32_t rows_per_rank);
+vcrt_result vcrt_get_stats(vcrt_stats* stats);
+
+/* Loads (or reloads) the tracer code object from a file; the analogue of
+ * CreateShaderStageFromFile. Returns VCRT_ERROR_INCOMPATIBLE_SHADER_BINARY when the file
+ * cannot be read or is not a gfx950 code object. Requires vcrt_begin. */
+vcrt_result vcrt_shader_load(const char* filename);
+
+/* Built-in scenes. */
+#define VCRT_SCENE_FINAL 0       /* SceneGenerator (481) + big three + ground = 485 spheres */
+#define VCRT_SCENE_THREE 1       /* big three + ground (globals.glsl:513-517) = 4 spheres   */
+#define VCRT_SCENE_RED 2         /* red Lambertian (0,1,0) r=1 + ground = 2 spheres         */
+#define VCRT_SCENE_STRESS4096 3  /* 4096 generated (grid [-33,33)^2) + big three + ground   */
+/* Writes up to cap spheres; returns the scene's sphere count, or a negative VkResult. */
+int32_t vcrt_scene_builtin(int32_t scene_id, vcrt_sphere* out, int32_t cap);
+/* SceneGenerator stdout, byte for byte. Returns the length (excluding NUL); writes up to cap-1
+ * bytes plus NUL when buf != NULL. */
+size_t vcrt_scene_generator_text(char* buf, size_t cap);
+
+/* Canonical math as used by the kernel (host evaluation), for tests and tools. */
+float vcrt_canonical_sin(float x);
+float vcrt_canonical_rand(float x, float y);
+
+const char* vcrt_result_string(vcrt_result r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

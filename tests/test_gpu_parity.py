@@ -1,0 +1,205 @@
+"""GPU parity: the gfx950 tracer (through the C ABI) against the CPU oracle.
+
+Bar (DESIGN.md "Parity"): bit-identical images and identical segment counts on every config
+the oracle finishes in seconds; at BASELINE sizes, bit-identical rows on an oracle-rendered
+row subset and per-channel RMS <= 1e-4 (north_star tolerance) over those rows.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import vulkancomputeraytracing_amd as vc
+from vulkancomputeraytracing_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+RMS_TOL = 1e-4  # north_star: per-channel RMS <= 1e-4 vs reference
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0, world=1,
+               stripe=16, frames=1, scene_arr=None):
+    desc = vc.RenderDesc(width=width, height=height, samples_per_pixel=spp, max_depth=depth,
+                         kernel_variant=variant, rank=rank, world_size=world,
+                         stripe_height=stripe, device=0)
+    with vc.Renderer(desc, scene_arr if scene_arr is not None else scene) as r:
+        for _ in range(frames):
+            r.draw_next_frame()
+        return r.read_framebuffer(), r.stats()
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def assert_bitwise(got, want, what=""):
+    if not np.array_equal(bits(got), bits(want)):
+        diff = np.argwhere(bits(got) != bits(want))
+        rms = np.sqrt(np.nanmean((got.astype(np.float64) - want) ** 2, axis=(0, 1)))
+        raise AssertionError(f"{what}: {len(diff)} words differ, first {diff[:5].tolist()}, "
+                             f"per-channel rms {rms}")
+
+
+CASES = [
+    # BASELINE config 1 (CPU plumbing config) run on the GPU too
+    ("red", 256, 144, 1, 1),
+    ("three", 200, 112, 8, 8),     # config 2 scene, reduced size
+    ("final", 160, 90, 4, 10),     # config 3 scene, reduced size
+    ("final", 96, 54, 2, 50),      # reference depth (MAX_RECURSION_LEVEL 50)
+    ("three", 37, 23, 3, 5),       # ragged sizes (not multiples of 8/16)
+    ("red", 1, 1, 5, 3),           # single pixel
+    ("final", 50, 1, 2, 10),       # single row
+]
+
+
+@pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
+@pytest.mark.parametrize("scene,w,h,spp,depth", CASES)
+def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene(scene))
+    got, st = gpu_render(scene, w, h, spp, depth, variant)
+    assert got.shape == want.shape
+    assert_bitwise(got, want, f"{scene} {w}x{h} spp{spp} d{depth} v{variant}")
+    assert st["segments"] == want_segs
+    assert st["kernel_variant"] == variant
+
+
+def test_golden_oracle_images():
+    from tests.golden.make_golden import IMAGES
+    data = np.load(os.path.join(GOLDEN, "oracle_images.npz"))
+    for name, scene, w, h, spp, depth in IMAGES:
+        got, st = gpu_render(scene, w, h, spp, depth)
+        assert_bitwise(got, data[name], name)
+        assert st["segments"] == int(data[name + "__segments"][0])
+
+
+def test_stress_scene_small(oracle):
+    w, h, spp, depth = 48, 27, 2, 10
+    want, segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("stress4096"))
+    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM):
+        got, st = gpu_render("stress4096", w, h, spp, depth, variant)
+        assert_bitwise(got, want, f"stress v{variant}")
+        assert st["segments"] == segs and st["nspheres"] == 4100
+
+
+def test_custom_scene_and_empty_scene(oracle):
+    custom = vc.make_spheres([((0, 0.5, -1), 0.5, (0.9, 0.1, 0.1), 2, 0.3),
+                              ((1, 0.5, -1), 0.5, (1, 1, 1), 3, 1.5),
+                              ((0, -100.5, -1), 100.0, (0.8, 0.8, 0.0), 1, 0.9)])
+    cfg = oracle.config(64, 40, 4, 8, lookfrom=(0, 1, 3), lookat=(0, 0.5, -1), vfov=40)
+    want, segs = oracle.render(cfg, custom)
+    desc = vc.RenderDesc(width=64, height=40, samples_per_pixel=4, max_depth=8,
+                         lookfrom=(0, 1, 3), lookat=(0, 0.5, -1), vfov=40, device=0)
+    with vc.Renderer(desc, custom) as r:
+        r.draw_next_frame()
+        assert_bitwise(r.read_framebuffer(), want, "custom")
+        assert r.stats()["segments"] == segs
+        # no spheres: every ray is sky
+        r.set_scene(custom[:0])
+        r.draw_next_frame()
+        got = r.read_framebuffer()
+    want0, _ = oracle.render(cfg, custom[:0])
+    assert_bitwise(got, want0, "empty scene")
+
+
+def test_depth_zero_fills_undefined_value():
+    got, st = gpu_render("final", 33, 17, 3, 0)
+    assert np.all(got[..., :3] == 0) and np.all(got[..., 3] == 1)
+    assert st["segments"] == 0
+
+
+def test_frames_are_identical(oracle):
+    # the reference re-renders the same deterministic frame every DrawNextFrame
+    desc = vc.RenderDesc(width=64, height=36, samples_per_pixel=2, max_depth=10, device=0)
+    with vc.Renderer(desc, "final") as r:
+        r.draw_next_frame()
+        a = r.read_framebuffer()
+        r.draw_next_frame()
+        b = r.read_framebuffer()
+        assert r.stats()["frames"] == 2
+    assert_bitwise(a, b, "frame 2 vs frame 1")
+
+
+@pytest.mark.parametrize("world,stripe", [(2, 16), (3, 16), (8, 16), (4, 5)])
+def test_sharded_stripes_reassemble_bitwise(world, stripe):
+    import torch
+    w, h, spp, depth = 72, 90, 2, 10
+    full, _ = gpu_render("final", w, h, spp, depth)
+    rows_per_rank = max(len(vc.rows_for_rank(h, stripe, world, r)) for r in range(world))
+    gathered = torch.zeros((world, rows_per_rank, w, 4), dtype=torch.float32, device="cuda:0")
+    segs = 0
+    for rank in range(world):
+        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world, stripe=stripe)
+        rows = vc.rows_for_rank(h, stripe, world, rank)
+        assert part.shape == (len(rows), w, 4)
+        assert_bitwise(part, full[rows], f"rank {rank}/{world}")
+        gathered[rank, :len(rows)] = torch.from_numpy(part).to("cuda:0")
+        segs += st["segments"]
+    frame = torch.empty((h, w, 4), dtype=torch.float32, device="cuda:0")
+    desc = vc.RenderDesc(width=w, height=h, world_size=world, stripe_height=stripe, device=0)
+    with vc.Renderer(desc) as r:
+        r.assemble_stripes(gathered.data_ptr(), frame.data_ptr(), rows_per_rank)
+    torch.cuda.synchronize()
+    assert_bitwise(frame.cpu().numpy(), full, "assembled")
+
+
+def test_render_into_external_device_buffer():
+    import torch
+    w, h = 40, 24
+    ref, _ = gpu_render("three", w, h, 2, 6)
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=2, max_depth=6, device=0)
+    buf = torch.full((h, w, 4), -1.0, dtype=torch.float32, device="cuda:0")
+    with vc.Renderer(desc, "three") as r:
+        r.set_framebuffer_device(buf.data_ptr(), buf.numel() * 4)
+        r.draw_next_frame()
+        torch.cuda.synchronize()
+        assert_bitwise(buf.cpu().numpy(), ref, "external buffer")
+        with pytest.raises(vc.VcrtError):
+            r.set_framebuffer_device(buf.data_ptr(), 16)  # too small
+
+
+def test_shader_load_from_file_and_errors(tmp_path):
+    desc = vc.RenderDesc(width=16, height=16, samples_per_pixel=1, max_depth=4, device=0)
+    with vc.Renderer(desc, "red") as r:
+        r.shader_load(N.CODE_OBJECT_PATH)
+        r.draw_next_frame()
+        with pytest.raises(vc.VcrtError) as e:
+            r.shader_load(str(tmp_path / "missing.hsaco"))
+        assert e.value.code == N.VK_ERROR_INCOMPATIBLE_SHADER_BINARY_EXT
+        junk = tmp_path / "junk.hsaco"
+        junk.write_bytes(b"\x7fELF not a code object" * 8)
+        with pytest.raises(vc.VcrtError) as e:
+            r.shader_load(str(junk))
+        assert e.value.code == N.VK_ERROR_INCOMPATIBLE_SHADER_BINARY_EXT
+        r.draw_next_frame()  # previous module still bound
+
+
+def test_reference_named_lifecycle():
+    vc.SetRenderDescription(vc.RenderDesc(width=32, height=18, samples_per_pixel=1,
+                                          max_depth=5, device=0))
+    vc.SetRenderScene(vc.builtin_scene("three"))
+    assert vc.BeginRenderingOperation() == vc.VK_SUCCESS
+    assert vc.DrawNextFrame() == vc.VK_SUCCESS
+    assert vc.EndRenderingOperation() == vc.VK_SUCCESS
+    assert vc.EndRenderingOperation() == vc.VK_SUCCESS
+    assert vc.DrawNextFrame() == vc.VK_ERROR_INITIALIZATION_FAILED
+    vc.SetRenderScene(None)
+
+
+def test_full_size_rows_subset_rms(oracle):
+    # BASELINE config 3 geometry (1920x1080, depth 10) at 16 spp; oracle renders every 90th row.
+    w, h, spp, depth = 1920, 1080, 16, 10
+    got, st = gpu_render("final", w, h, spp, depth)
+    rows = range(7, h, 90)
+    want, _ = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("final"), rows=rows)
+    sel = list(rows)
+    g, o = got[sel].astype(np.float64), want[sel].astype(np.float64)
+    rms = np.sqrt(((g - o) ** 2).mean(axis=(0, 1)))
+    assert np.all(rms[:3] <= RMS_TOL), rms
+    assert_bitwise(got[sel], want[sel], "full-size row subset")
+    # size-independent properties of the whole frame
+    assert np.all(got[..., 3] == 1.0)
+    assert np.all(np.isfinite(got)) and np.all(got[..., :3] >= 0)
+    assert st["samples"] == w * h * spp
+    assert st["segments"] >= w * h * spp  # at least one segment per sample

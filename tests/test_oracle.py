@@ -1,0 +1,147 @@
+"""The CPU oracle pinned against the reference: SceneGenerator output (golden vectors from the
+reference's own SceneGenerator.cpp compiled here), math KATs and the camera scalars, plus the
+committed oracle images (regression pins). SURVEY.md section 8(c)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests import oracle_py
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def golden_meta():
+    with open(os.path.join(GOLDEN, "scene_generator_stdout.json")) as f:
+        return json.load(f)
+
+
+def test_scene_generator_text_matches_reference_hash(oracle):
+    text = oracle.scene_generator_text()
+    meta = golden_meta()
+    assert len(text) == meta["bytes"]
+    assert hashlib.sha256(text).hexdigest() == meta["sha256"]
+
+
+@pytest.mark.skipif(not os.path.exists(oracle_py.REF_SCENEGEN),
+                    reason="reference SceneGenerator not built (needs /root/reference)")
+def test_scene_generator_text_matches_reference_binary(oracle):
+    import subprocess
+    ref = subprocess.run([oracle_py.REF_SCENEGEN], capture_output=True, check=True).stdout
+    assert oracle.scene_generator_text() == ref
+
+
+def test_scene_spheres_match_reference_values(oracle):
+    want = np.load(os.path.join(GOLDEN, "scene_generator_spheres.npy"))
+    got = oracle.random_spheres(-11, 11)
+    assert len(got) == len(want) == 481
+    flat = np.concatenate([got["center"], got["radius"][:, None], got["colour"],
+                           got["texture"]], axis=1)
+    assert np.array_equal(flat.view(np.uint32), want.view(np.uint32))
+    # counts from SURVEY.md 3.4: 371 Lambertian, 74 metal, 36 glass
+    kinds = got["texture"][:, 0]
+    assert (kinds == 1).sum() == 371 and (kinds == 2).sum() == 74 and (kinds == 3).sum() == 36
+
+
+def test_scene_sizes(oracle):
+    assert len(oracle.scene("final")) == 485
+    assert len(oracle.scene("three")) == 4
+    assert len(oracle.scene("red")) == 2
+    s = oracle.scene("stress4096")
+    assert len(s) == 4100
+    # same generator rules on the wider grid: every generated sphere is small and on the floor
+    assert np.all(s["radius"][:4096] == np.float32(0.2))
+    assert np.all(s["center"][:4096, 1] == np.float32(0.2))
+
+
+RAND_KAT = [0.0, 0.6875, 0.467773438, 0.068359375, 0.296875, 0.6875, 0.994140625, 0.947265625,
+            0.8046875, 0.265625]
+
+
+def test_rand_known_answers(oracle):
+    # rand(i,i) for i=0..9, 1023, 1024 (fp32, no contraction)
+    for i, want in enumerate(RAND_KAT):
+        assert oracle.rand(float(i), float(i)) == pytest.approx(want, abs=5e-10)
+    assert oracle.rand(1023.0, 1023.0) == pytest.approx(0.419921875, abs=5e-10)
+    assert oracle.rand(1024.0, 1024.0) == pytest.approx(0.838012695, abs=5e-10)
+
+
+def _correctly_rounded_sin(x32: np.ndarray) -> np.ndarray:
+    return np.sin(x32.astype(np.float64)).astype(np.float32)
+
+
+@pytest.mark.parametrize("lo,hi", [(-10.0, 10.0), (-1e5, 1e5), (1e5, 1e8), (-3e38, 3e38)])
+def test_canonical_sin_is_correctly_rounded(oracle, lo, hi):
+    rng = np.random.default_rng(int(abs(lo)) % 1000 + 7)
+    if hi > 1e9:
+        xs = (rng.standard_normal(20000) * 10.0 ** rng.uniform(-3, 38, 20000)).astype(np.float32)
+        xs = xs[np.isfinite(xs)]
+    else:
+        xs = rng.uniform(lo, hi, 20000).astype(np.float32)
+    want = _correctly_rounded_sin(xs)
+    got = np.array([oracle.sin(float(x)) for x in xs], dtype=np.float32)
+    assert np.array_equal(got, want)
+
+
+def test_canonical_sin_special_values(oracle):
+    assert oracle.sin(0.0) == 0.0
+    assert np.isnan(oracle.sin(float("inf")))
+    assert np.isnan(oracle.sin(float("nan")))
+    # exponent boundary between the two reductions (2^20)
+    for x in [2.0 ** 20, np.nextafter(np.float32(2.0 ** 20), np.float32(0)), 2.0 ** 20 + 1]:
+        x = float(np.float32(x))
+        assert oracle.sin(x) == _correctly_rounded_sin(np.array([x], np.float32))[0]
+
+
+def test_camera_scalars(oracle):
+    cam = oracle.camera(oracle.config(1280, 720, 1, 50))
+    # focal=13.490738, vh=vw=4.757562 for every 16:9 config
+    assert cam[12] == pytest.approx(13.490738, abs=1e-6)
+    assert cam[13] == pytest.approx(4.757562, abs=1e-6)
+    assert cam[14] == cam[13]  # integer IMAGE_WIDTH/IMAGE_HEIGHT == 1
+    # delta_u divided by H, not W (shader.comp:35): |du| = vw / H
+    du = cam[3:6]
+    assert np.sqrt((du.astype(np.float64) ** 2).sum()) == pytest.approx(cam[14] / 720, rel=1e-6)
+
+
+def test_depth_one_red_scene_semantics(oracle):
+    # BASELINE config 1 at reduced size: with depth 1 every hit returns the undefined value
+    # (canonical 0) and every miss returns the sky term.
+    img, segs = oracle.render(oracle.config(64, 36, 1, 1), oracle.scene("red"))
+    assert segs == 64 * 36
+    assert np.all(img[..., 3] == 1.0)
+    rgb = img[..., :3]
+    hit = np.all(rgb == 0.0, axis=-1)
+    assert 0 < hit.sum() < hit.size
+    sky = rgb[~hit]
+    assert np.all(sky[:, 2] == 1.0) or np.all(sky > 0)
+
+
+def test_oracle_images_regression(oracle):
+    from tests.golden.make_golden import IMAGES
+    data = np.load(os.path.join(GOLDEN, "oracle_images.npz"))
+    for name, scene, w, h, spp, depth in IMAGES:
+        img, segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene(scene))
+        assert np.array_equal(img.view(np.uint32), data[name].view(np.uint32)), name
+        assert segs == int(data[name + "__segments"][0]), name
+
+
+def test_oracle_row_subset_and_threads_are_deterministic(oracle):
+    cfg = oracle.config(40, 24, 2, 6)
+    scene = oracle.scene("three")
+    full1, s1 = oracle.render(cfg, scene, threads=1)
+    full8, s8 = oracle.render(cfg, scene, threads=8)
+    assert np.array_equal(full1.view(np.uint32), full8.view(np.uint32)) and s1 == s8
+    sub, _ = oracle.render(cfg, scene, rows=range(3, 24, 5))
+    for y in range(24):
+        if y >= 3 and (y - 3) % 5 == 0:
+            assert np.array_equal(sub[y].view(np.uint32), full1[y].view(np.uint32))
+        else:
+            assert not sub[y].any()
+
+
+def test_oracle_rejects_bad_config(oracle):
+    with pytest.raises(ValueError):
+        oracle.render(oracle.config(8, 8, 0, 1), oracle.scene("red"))

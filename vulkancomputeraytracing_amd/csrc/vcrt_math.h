@@ -1,0 +1,190 @@
+// vcrt_math.h -- canonical fp32 math shared by the gfx950 tracer kernel and the C++ host
+// (camera setup, jitter table). Every function is one fixed sequence of correctly rounded
+// IEEE operations, so the device and the host (and the CPU oracle, which restates the same
+// definitions independently in oracle/vcrt_oracle.c) agree bit for bit.
+//
+// The GLSL built-ins these stand for are driver-defined in the reference
+// (shaders/include/functions.glsl, textures.glsl); the canonical choices are listed in
+// DESIGN.md "Canonical math". Compile with -ffp-contract=off; never with fast-math.
+#pragma once
+
+#include <cstdint>
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define VCRT_HD __host__ __device__ __forceinline__
+#else
+#define VCRT_HD inline
+#endif
+
+namespace vcrt {
+
+struct f3 {
+    float x, y, z;
+};
+
+VCRT_HD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+VCRT_HD f3 add(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+VCRT_HD f3 sub(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+VCRT_HD f3 mul(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+VCRT_HD f3 scale(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+VCRT_HD f3 divs(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+VCRT_HD f3 neg(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+// GLSL dot: (x*x' + y*y') + z*z'
+VCRT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+VCRT_HD float length(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+// GLSL normalize(x) = x / length(x)
+VCRT_HD f3 normalize(f3 a) { return divs(a, length(a)); }
+// GLSL cross(x,y) = (x1*y2 - y1*x2, x2*y0 - y2*x0, x0*y1 - y0*x1)
+VCRT_HD f3 cross(f3 a, f3 b) {
+    return f3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+// GLSL reflect(I,N) = I - 2.0*dot(N,I)*N
+VCRT_HD f3 reflect(f3 i, f3 n) { return sub(i, scale(2.0f * dot(n, i), n)); }
+VCRT_HD float radians(float deg) { return deg * 0.017453292519943295f; }
+
+// ---------------------------------------------------------------------------------------
+// canonical sin: fp32 argument widened to double, reduced to [-pi/4, pi/4] (Cody-Waite for
+// |x| < 2^20, exact 96-bit integer reduction by 2/pi above), fdlibm kernels, one rounding.
+// Equals the correctly rounded sinf except in astronomically rare double-rounding ties
+// (tests/test_oracle.py checks it against float64 sin on 4e5 arguments).
+
+VCRT_HD double ksin(double x) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x;
+    double v = z * x;
+    double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x + v * (S1 + z * r);
+}
+
+VCRT_HD double kcos(double x) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x;
+    double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    double hz = 0.5 * z;
+    double w = 1.0 - hz;
+    return w + (((1.0 - w) - hz) + z * r);
+}
+
+// 32-bit windows of 2/pi = 0.A2F9836E 4E441529 ..., with one zero word in front.
+VCRT_HD uint32_t two_over_pi_word(int i) {
+    switch (i) {
+        case 0: return 0x00000000u;
+        case 1: return 0xA2F9836Eu;
+        case 2: return 0x4E441529u;
+        case 3: return 0xFC2757D1u;
+        case 4: return 0xF534DDC0u;
+        case 5: return 0xDB629599u;
+        case 6: return 0x3C439041u;
+        case 7: return 0xFE5163ABu;
+        default: return 0xDEBBC561u;
+    }
+}
+
+VCRT_HD uint32_t two_over_pi_window(int bitpos) {
+    int wi = bitpos >> 5, sh = bitpos & 31;
+    uint32_t hi = two_over_pi_word(wi);
+    if (sh == 0) return hi;
+    return (hi << sh) | (two_over_pi_word(wi + 1) >> (32 - sh));
+}
+
+// Large-argument reduction (|x| >= 2^20): r in [-pi/4, pi/4), quadrant q in [0,4).
+VCRT_HD double reduce_large(uint32_t bits, int* q_out) {
+    uint32_t e = (bits >> 23) & 0xFFu;
+    uint32_t m = (bits & 0x7FFFFFu) | 0x800000u;
+    int b = (int)e - 150 + 30;
+    uint64_t w0 = two_over_pi_window(b), w1 = two_over_pi_window(b + 32),
+             w2 = two_over_pi_window(b + 64);
+    uint64_t p2 = (uint64_t)m * w2, p1 = (uint64_t)m * w1, p0 = (uint64_t)m * w0;
+    uint64_t t = (p2 >> 32) + (p1 & 0xFFFFFFFFu);
+    uint32_t mid = (uint32_t)t;
+    t = (t >> 32) + (p1 >> 32) + (p0 & 0xFFFFFFFFu);
+    uint32_t hi = (uint32_t)t;
+    uint64_t frac = ((uint64_t)(hi & 0x3FFFFFFFu) << 34) | ((uint64_t)mid << 2) |
+                    ((uint64_t)(uint32_t)p2 >> 30);
+    int q = (int)(hi >> 30);
+    int64_t sf = (int64_t)frac;
+    if (sf < 0) q += 1;
+    double r = ((double)sf * 0x1p-64) * 1.57079632679489661923e+00;
+    if (bits >> 31) {
+        r = -r;
+        q = -q;
+    }
+    *q_out = q & 3;
+    return r;
+}
+
+VCRT_HD float sin_canonical(float xf) {
+    uint32_t bits = __builtin_bit_cast(uint32_t, xf);
+    uint32_t e = (bits >> 23) & 0xFFu;
+    if (e == 0xFFu) return xf - xf;
+    double r;
+    int q;
+    if (e < 147u) {
+        double x = (double)xf;
+        double k = __builtin_rint(x * 6.36619772367581382433e-01);
+        r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+        q = (int)((int64_t)k & 3);
+    } else {
+        r = reduce_large(bits, &q);
+    }
+    double s = (q & 1) ? kcos(r) : ksin(r);
+    if (q & 2) s = -s;
+    return (float)s;
+}
+
+// functions.glsl:10-12  rand(co) = fract(sin(dot(co, vec2(12.9898,78.233))) * 43758.5453)
+VCRT_HD float rand2(float x, float y) {
+    float arg = x * 12.9898f + y * 78.233f;
+    float p = sin_canonical(arg) * 43758.5453f;
+    return p - __builtin_floorf(p);
+}
+
+// functions.glsl:58-62 with canonical pow(x,5): NaN for x < 0 (GLSL leaves it undefined)
+VCRT_HD float schlick(float cosine, float ior) {
+    float r0 = (1.0f - ior) / (1.0f + ior);
+    r0 = r0 * r0;
+    float x = 1.0f - cosine;
+    float p5 = (x < 0.0f) ? __builtin_nanf("") : ((x * x) * (x * x)) * x;
+    return r0 + (1.0f - r0) * p5;
+}
+
+// ---------------------------------------------------------------------------------------
+// Camera: shader.comp:18-39, computed once on the host (it is uniform per dispatch).
+
+struct Camera {
+    f3 pixel00, delta_u, delta_v, center;
+    float focal_length, viewport_height, viewport_width;
+};
+
+inline Camera make_camera(int width, int height, f3 lookfrom, f3 lookat, f3 vup, float vfov,
+                          double (*tan_fn)(double)) {
+    Camera c;
+    c.center = lookfrom;
+    c.focal_length = length(sub(lookfrom, lookat));
+    float theta = radians(vfov);
+    float h = (float)tan_fn((double)(theta / 2.0f));
+    c.viewport_height = 2.0f * h * c.focal_length;
+    c.viewport_width = c.viewport_height * (float)(width / height);  // integer division
+    f3 w = normalize(sub(lookfrom, lookat));
+    f3 u = normalize(cross(vup, w));
+    f3 v = cross(w, u);
+    f3 viewport_u = scale(c.viewport_width, u);
+    f3 viewport_v = scale(c.viewport_height, neg(v));
+    c.delta_u = divs(viewport_u, (float)height);  // divided by H (shader.comp:35)
+    c.delta_v = divs(viewport_v, (float)height);
+    f3 ul = sub(sub(sub(c.center, scale(c.focal_length, w)), divs(viewport_u, 2.0f)),
+                divs(viewport_v, 2.0f));
+    c.pixel00 = add(ul, scale(0.5f, add(c.delta_u, c.delta_v)));
+    return c;
+}
+
+}  // namespace vcrt

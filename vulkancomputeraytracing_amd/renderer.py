@@ -1,0 +1,179 @@
+"""Python mirror of the reference's Renderer lifecycle (include/Renderer.hpp:14-20).
+
+``BeginRenderingOperation`` / ``DrawNextFrame`` / ``EndRenderingOperation`` keep the reference's
+names and VkResult return convention (0 = VK_SUCCESS, negative = error). ``RenderDesc`` carries
+what the reference fixed at compile time (globals.glsl:9-24). ``Renderer`` is the same lifecycle
+as a context manager that raises on error. Everything goes through libvcrt.so (the C ABI of
+include/vcrt.h); the compute runs in the gfx950 kernels of vcrt_tracer.hsaco.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as N
+from .scene import SPHERE_DTYPE, builtin_scene
+
+
+@dataclass
+class RenderDesc:
+    width: int = 1280               # IMAGE_WIDTH  (globals.glsl:16)
+    height: int = 720               # IMAGE_HEIGHT (globals.glsl:17)
+    samples_per_pixel: int = 1      # SAMPLES_PER_PIXEL (globals.glsl:9-13)
+    max_depth: int = 50             # MAX_RECURSION_LEVEL (globals.glsl:14)
+    lookfrom: tuple = (13.0, 2.0, 3.0)   # globals.glsl:21-24
+    lookat: tuple = (0.0, 0.0, 0.0)
+    vup: tuple = (0.0, 1.0, 0.0)
+    vfov: float = 20.0
+    device: int = -1
+    rank: int = 0
+    world_size: int = 1
+    stripe_height: int = 16
+    kernel_variant: int = N.KERNEL_AUTO
+    blocks_per_cu: int = 0
+    code_object_path: str | None = None
+    _path_keepalive: bytes | None = field(default=None, repr=False)
+
+    def to_c(self) -> N.vcrt_render_desc:
+        d = N.vcrt_render_desc()
+        N.lib().vcrt_default_desc(ctypes.byref(d))
+        d.width, d.height = self.width, self.height
+        d.samples_per_pixel, d.max_depth = self.samples_per_pixel, self.max_depth
+        d.camera.lookfrom[:] = [float(v) for v in self.lookfrom]
+        d.camera.lookat[:] = [float(v) for v in self.lookat]
+        d.camera.vup[:] = [float(v) for v in self.vup]
+        d.camera.vfov = float(self.vfov)
+        d.device = self.device
+        d.rank, d.world_size = self.rank, self.world_size
+        d.stripe_height = self.stripe_height
+        d.kernel_variant = self.kernel_variant
+        d.blocks_per_cu = self.blocks_per_cu
+        if self.code_object_path:
+            self._path_keepalive = self.code_object_path.encode()
+            d.code_object_path = self._path_keepalive
+        return d
+
+
+def rows_for_rank(height: int, stripe: int, world: int, rank: int) -> list[int]:
+    """Global rows owned by `rank`: stripe s = y // stripe belongs to rank s % world."""
+    return [y for y in range(height) if (y // stripe) % world == rank]
+
+
+# ---- reference-named lifecycle (VkResult codes, no exceptions) ----------------------------
+
+_desc = RenderDesc()
+_scene: np.ndarray | None = None
+
+
+def SetRenderDescription(desc: RenderDesc) -> int:
+    global _desc
+    _desc = desc
+    return N.VK_SUCCESS
+
+
+def SetRenderScene(spheres) -> int:
+    global _scene
+    _scene = None if spheres is None else np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+    return N.VK_SUCCESS
+
+
+def BeginRenderingOperation() -> int:
+    lib = N.lib()
+    d = _desc.to_c()
+    r = lib.vcrt_begin(ctypes.byref(d))
+    if r == N.VK_SUCCESS and _scene is not None:
+        r = lib.vcrt_set_scene(_scene.ctypes.data_as(ctypes.POINTER(N.vcrt_sphere)), len(_scene))
+        if r != N.VK_SUCCESS:
+            lib.vcrt_end()
+    return r
+
+
+def DrawNextFrame() -> int:
+    return N.lib().vcrt_draw_next_frame()
+
+
+def EndRenderingOperation() -> int:
+    return N.lib().vcrt_end()
+
+
+# ---- the same lifecycle as an object --------------------------------------------------------
+
+class Renderer:
+    """Begin on construction / __enter__, End on close / __exit__; raises VcrtError."""
+
+    def __init__(self, desc: RenderDesc | None = None, scene=None):
+        self.desc = desc or RenderDesc()
+        self._lib = N.lib()
+        self._c_desc = self.desc.to_c()
+        N.check("vcrt_begin", self._lib.vcrt_begin(ctypes.byref(self._c_desc)))
+        self._open = True
+        if scene is not None:
+            self.set_scene(scene)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def close(self):
+        if getattr(self, "_open", False):
+            self._lib.vcrt_end()
+            self._open = False
+
+    def set_scene(self, scene) -> None:
+        arr = builtin_scene(scene) if isinstance(scene, (str, int)) else scene
+        arr = np.ascontiguousarray(arr, dtype=SPHERE_DTYPE)
+        self._scene = arr
+        N.check("vcrt_set_scene", self._lib.vcrt_set_scene(
+            arr.ctypes.data_as(ctypes.POINTER(N.vcrt_sphere)), len(arr)))
+
+    def draw_next_frame(self) -> None:
+        N.check("vcrt_draw_next_frame", self._lib.vcrt_draw_next_frame())
+
+    @property
+    def local_rows(self) -> int:
+        v = ctypes.c_int32()
+        N.check("vcrt_local_rows", self._lib.vcrt_local_rows(ctypes.byref(v)))
+        return v.value
+
+    def read_framebuffer(self) -> np.ndarray:
+        """Rank-local framebuffer as float32 [local_rows, width, 4] (rgba32f, top row first)."""
+        out = np.empty((self.local_rows, self.desc.width, 4), dtype=np.float32)
+        N.check("vcrt_read_framebuffer", self._lib.vcrt_read_framebuffer(
+            out.ctypes.data_as(ctypes.c_void_p), out.size))
+        return out
+
+    def framebuffer_device(self) -> tuple[int, int]:
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        N.check("vcrt_framebuffer_device",
+                self._lib.vcrt_framebuffer_device(ctypes.byref(p), ctypes.byref(n)))
+        return p.value or 0, n.value
+
+    def set_framebuffer_device(self, ptr: int | None, nbytes: int = 0) -> None:
+        N.check("vcrt_set_framebuffer_device",
+                self._lib.vcrt_set_framebuffer_device(ctypes.c_void_p(ptr or None), nbytes))
+
+    def assemble_stripes(self, gathered_ptr: int, frame_ptr: int, rows_per_rank: int) -> None:
+        d = self.desc
+        N.check("vcrt_assemble_stripes", self._lib.vcrt_assemble_stripes(
+            ctypes.c_void_p(gathered_ptr), ctypes.c_void_p(frame_ptr), d.width, d.height,
+            d.world_size, d.stripe_height, rows_per_rank))
+
+    def shader_load(self, path: str) -> None:
+        N.check("vcrt_shader_load", self._lib.vcrt_shader_load(path.encode()))
+
+    def stats(self) -> dict:
+        s = N.vcrt_stats()
+        N.check("vcrt_get_stats", self._lib.vcrt_get_stats(ctypes.byref(s)))
+        return {name: getattr(s, name) for name, _ in N.vcrt_stats._fields_}
+
+
+def render(desc: RenderDesc, scene="final", frames: int = 1) -> tuple[np.ndarray, dict]:
+    """Convenience: Begin, draw `frames` frames, read the rank-local framebuffer, End."""
+    with Renderer(desc, scene) as r:
+        for _ in range(frames):
+            r.draw_next_frame()
+        return r.read_framebuffer(), r.stats()

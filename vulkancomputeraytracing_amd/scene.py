@@ -1,0 +1,60 @@
+"""SceneGenerator surface (reference: SceneGenerator.cpp:10-56, globals.glsl:29-518).
+
+Scenes are numpy structured arrays with the GLSL ``struct sphere`` layout
+(structures.glsl:10-16): center[3], radius, colour[3], texture[3] -- 40 bytes per sphere.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+SPHERE_DTYPE = np.dtype([
+    ("center", np.float32, (3,)),
+    ("radius", np.float32),
+    ("colour", np.float32, (3,)),
+    ("texture", np.float32, (3,)),
+])
+assert SPHERE_DTYPE.itemsize == ctypes.sizeof(N.vcrt_sphere) == 40
+
+SCENES = {
+    "final": N.SCENE_FINAL,        # 481 generated + big three + ground = 485
+    "three": N.SCENE_THREE,        # big three + ground (globals.glsl:513-517)
+    "red": N.SCENE_RED,            # red Lambertian sphere + ground (BASELINE config 1)
+    "stress4096": N.SCENE_STRESS4096,  # 4096 generated + big three + ground = 4100
+}
+
+
+def builtin_scene(name_or_id) -> np.ndarray:
+    """Spheres of a built-in scene, in world[] order."""
+    sid = SCENES[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)
+    lib = N.lib()
+    n = lib.vcrt_scene_builtin(sid, None, 0)
+    if n < 0:
+        raise N.VcrtError("vcrt_scene_builtin", n)
+    arr = np.zeros(n, dtype=SPHERE_DTYPE)
+    got = lib.vcrt_scene_builtin(sid, arr.ctypes.data_as(ctypes.POINTER(N.vcrt_sphere)), n)
+    assert got == n
+    return arr
+
+
+def scene_generator_text() -> str:
+    """The SceneGenerator executable's stdout, byte for byte."""
+    lib = N.lib()
+    n = lib.vcrt_scene_generator_text(None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.vcrt_scene_generator_text(buf, n + 1)
+    return buf.raw[:n].decode()
+
+
+def make_spheres(rows) -> np.ndarray:
+    """Build a scene from (center(3), radius, colour(3), material id, param) tuples."""
+    arr = np.zeros(len(rows), dtype=SPHERE_DTYPE)
+    for i, (c, r, col, mat, param) in enumerate(rows):
+        arr[i]["center"] = c
+        arr[i]["radius"] = r
+        arr[i]["colour"] = col
+        arr[i]["texture"] = (mat, param, 0.0)
+    return arr
