@@ -85,6 +85,10 @@ typedef struct vcrt_render_desc {
     int32_t stripe_height; /* rows per interleaved stripe; 0 = 16 */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
+    int32_t accumulate_chunk; /* samples per work item (0 = 32). A pixel's samples are summed
+                                 in order within a chunk and the chunk sums in chunk order;
+                                 >= samples_per_pixel reproduces the reference's sequential
+                                 sum (shader.comp:46-54) exactly. */
     const char* code_object_path; /* NULL = vcrt_tracer.hsaco next to libvcrt.so, then embedded */
 } vcrt_render_desc;
 
@@ -94,11 +98,15 @@ typedef struct vcrt_stats {
     uint64_t samples;      /* local_rows * width * spp */
     double kernel_ms;      /* tracer kernel time, HIP events on the render stream */
     double frame_ms;       /* host wall time of the last vcrt_draw_next_frame */
+    double resolve_ms;     /* chunk-sum resolve kernel time (0 when one chunk) */
     int32_t frames;        /* frames drawn since vcrt_begin */
     int32_t grid_blocks, block_threads, kernel_variant;
     int32_t local_rows;    /* rows of this rank's packed framebuffer */
     int32_t nspheres;
     uint32_t lds_bytes;
+    int32_t accumulate_chunk; /* samples per work item in effect */
+    uint64_t debug[8]; /* diagnostics (VCRT_DEBUG_STATS=1): wave-iterations, active-lane sum,
+                          hit groups, fetches, last/first wave end time, sum end time, waves */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

@@ -325,13 +325,21 @@ static void render_row(render_job* job, int y, uint64_t* segs) {
     v3 center = V(job->cam[9], job->cam[10], job->cam[11]);
     for (int x = 0; x < cfg->width; x++) {
         v3 pc = vadd(vadd(p00, vscale((float)x, du)), vscale((float)y, dv));
+        const int chunk =
+            (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= cfg->spp) ? cfg->spp
+                                                                               : cfg->accumulate_chunk;
         v3 acc = V(0.0f, 0.0f, 0.0f);
-        for (int i = 0; i < cfg->spp; i++) {
-            float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
-            v3 rs = vadd(vscale(jx, du), vscale(jy, dv));
-            v3 ps = vadd(pc, rs);
-            v3 dir = vsub(ps, center);
-            acc = vadd(acc, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
+        for (int c0 = 0; c0 < cfg->spp; c0 += chunk) {
+            v3 part = V(0.0f, 0.0f, 0.0f);
+            const int c1 = c0 + chunk < cfg->spp ? c0 + chunk : cfg->spp;
+            for (int i = c0; i < c1; i++) {
+                float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
+                v3 rs = vadd(vscale(jx, du), vscale(jy, dv));
+                v3 ps = vadd(pc, rs);
+                v3 dir = vsub(ps, center);
+                part = vadd(part, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
+            }
+            acc = vadd(acc, part); /* one chunk: 0 + part == part, the sequential sum */
         }
         float* px = job->rgba + ((size_t)y * cfg->width + x) * 4;
         px[0] = acc.x / (float)cfg->spp;

@@ -34,6 +34,10 @@ typedef struct oracle_config {
     int32_t width, height, spp, max_depth;
     float lookfrom[3], lookat[3], vup[3];
     float vfov;
+    /* Accumulation order. 0 or >= spp: the reference's sequential sum (shader.comp:46-54).
+     * K < spp: samples summed sequentially within chunks of K, chunk sums then added in chunk
+     * order (the order the GPU uses when it splits a pixel's samples into work items). */
+    int32_t accumulate_chunk;
 } oracle_config;
 
 /* Canonical math (see DESIGN.md "canonical math"). */

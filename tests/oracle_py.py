@@ -29,6 +29,7 @@ class OracleConfig(ctypes.Structure):
         ("spp", ctypes.c_int32), ("max_depth", ctypes.c_int32),
         ("lookfrom", ctypes.c_float * 3), ("lookat", ctypes.c_float * 3),
         ("vup", ctypes.c_float * 3), ("vfov", ctypes.c_float),
+        ("accumulate_chunk", ctypes.c_int32),
     ]
 
 
@@ -72,8 +73,9 @@ class Oracle:
 
     @staticmethod
     def config(width, height, spp, max_depth, lookfrom=(13, 2, 3), lookat=(0, 0, 0),
-               vup=(0, 1, 0), vfov=20.0) -> OracleConfig:
+               vup=(0, 1, 0), vfov=20.0, chunk=0) -> OracleConfig:
         c = OracleConfig()
+        c.accumulate_chunk = chunk
         c.width, c.height, c.spp, c.max_depth = width, height, spp, max_depth
         c.lookfrom[:] = [float(v) for v in lookfrom]
         c.lookat[:] = [float(v) for v in lookat]

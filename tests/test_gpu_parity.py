@@ -20,10 +20,10 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0, world=1,
-               stripe=16, frames=1, scene_arr=None):
+               stripe=16, frames=1, scene_arr=None, chunk=0):
     desc = vc.RenderDesc(width=width, height=height, samples_per_pixel=spp, max_depth=depth,
                          kernel_variant=variant, rank=rank, world_size=world,
-                         stripe_height=stripe, device=0)
+                         stripe_height=stripe, device=0, accumulate_chunk=chunk)
     with vc.Renderer(desc, scene_arr if scene_arr is not None else scene) as r:
         for _ in range(frames):
             r.draw_next_frame()
@@ -63,6 +63,27 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     assert_bitwise(got, want, f"{scene} {w}x{h} spp{spp} d{depth} v{variant}")
     assert st["segments"] == want_segs
     assert st["kernel_variant"] == variant
+
+
+@pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk", [
+    ("final", 64, 36, 64, 10, 16),   # 4 chunks
+    ("final", 48, 30, 40, 10, 0),    # default chunk 32: chunks of 32 + 8 (ragged)
+    ("three", 72, 40, 96, 8, 7),     # 14 chunks, last one of 5
+    ("final", 40, 24, 33, 10, 33),   # one chunk = the reference's sequential order
+])
+def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, variant):
+    k = vc.renderer.effective_chunk(spp, chunk)
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
+    got, st = gpu_render(scene, w, h, spp, depth, variant, chunk=chunk)
+    assert st["accumulate_chunk"] == k
+    assert_bitwise(got, want, f"{scene} spp{spp} chunk{k}")
+    assert st["segments"] == want_segs
+    # the chunked order stays within the north_star tolerance of the sequential order
+    seq, _ = oracle.render(oracle.config(w, h, spp, depth), oracle.scene(scene))
+    rms = np.sqrt(((got.astype(np.float64) - seq) ** 2).mean(axis=(0, 1)))
+    assert np.all(rms <= RMS_TOL), rms
+    assert np.all(rms <= 1e-6), rms  # in practice a few ulps
 
 
 def test_golden_oracle_images():

@@ -145,3 +145,16 @@ def test_oracle_row_subset_and_threads_are_deterministic(oracle):
 def test_oracle_rejects_bad_config(oracle):
     with pytest.raises(ValueError):
         oracle.render(oracle.config(8, 8, 0, 1), oracle.scene("red"))
+
+
+def test_chunked_order_is_close_to_sequential(oracle):
+    cfg_seq = oracle.config(32, 18, 64, 10)
+    cfg_chk = oracle.config(32, 18, 64, 10, chunk=16)
+    a, sa = oracle.render(cfg_seq, oracle.scene("final"))
+    b, sb = oracle.render(cfg_chk, oracle.scene("final"))
+    assert sa == sb  # same paths, only the summation order differs
+    rms = np.sqrt(((a.astype(np.float64) - b) ** 2).mean(axis=(0, 1)))
+    assert np.all(rms < 1e-6), rms
+    # chunk >= spp is exactly the sequential order
+    c, _ = oracle.render(oracle.config(32, 18, 64, 10, chunk=64), oracle.scene("final"))
+    assert np.array_equal(a.view(np.uint32), c.view(np.uint32))

@@ -71,6 +71,7 @@ class vcrt_render_desc(ctypes.Structure):
         ("stripe_height", ctypes.c_int32),
         ("kernel_variant", ctypes.c_int32),
         ("blocks_per_cu", ctypes.c_int32),
+        ("accumulate_chunk", ctypes.c_int32),
         ("code_object_path", ctypes.c_char_p),
     ]
 
@@ -82,6 +83,7 @@ class vcrt_stats(ctypes.Structure):
         ("samples", ctypes.c_uint64),
         ("kernel_ms", ctypes.c_double),
         ("frame_ms", ctypes.c_double),
+        ("resolve_ms", ctypes.c_double),
         ("frames", ctypes.c_int32),
         ("grid_blocks", ctypes.c_int32),
         ("block_threads", ctypes.c_int32),
@@ -89,6 +91,8 @@ class vcrt_stats(ctypes.Structure):
         ("local_rows", ctypes.c_int32),
         ("nspheres", ctypes.c_int32),
         ("lds_bytes", ctypes.c_uint32),
+        ("accumulate_chunk", ctypes.c_int32),
+        ("debug", ctypes.c_uint64 * 8),
     ]
 
 
@@ -119,6 +123,20 @@ SIGNATURES = {
 _lib = None
 
 
+def _share_torch_hip_runtime() -> None:
+    """One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (SONAME
+    libamdhip64.so.7, the same as /opt/rocm's). If it is loaded first, libvcrt.so's
+    DT_NEEDED libamdhip64.so.7 binds to it and torch tensors, streams and RCCL share one runtime
+    with the tracer; loaded the other way round the process would hold two HIP/HSA runtimes."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        return
+    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if os.path.exists(torch_lib):
+        ctypes.CDLL(torch_lib, mode=ctypes.RTLD_GLOBAL)
+
+
 def lib() -> ctypes.CDLL:
     """Load libvcrt.so (fails loudly when it has not been built)."""
     global _lib
@@ -127,6 +145,8 @@ def lib() -> ctypes.CDLL:
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with `make -C {HERE}` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
+        if os.environ.get("VCRT_SYSTEM_HIP", "0") != "1":
+            _share_torch_hip_runtime()
         handle = ctypes.CDLL(LIB_PATH)
         for name, (restype, argtypes) in SIGNATURES.items():
             fn = getattr(handle, name)

@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -30,6 +31,7 @@ namespace {
 using vcrt::to_vk;
 
 constexpr size_t kCounterBytes = 256;  // work counter (u32) + segment counter (u64), padded
+constexpr int32_t kDefaultChunk = 32;  // samples per work item
 
 struct RendererState {
     bool begun = false;
@@ -38,15 +40,25 @@ struct RendererState {
     int num_cus = 0;
     size_t max_lds = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr, ev_resolve = nullptr;
     VkPipelineShaderStageCreateInfo stage{};
     hipFunction_t k_trace_lds = nullptr, k_trace_smem = nullptr, k_assemble = nullptr,
-                  k_fill = nullptr;
+                  k_fill = nullptr, k_trace_lds_stats = nullptr, k_trace_smem_stats = nullptr,
+                  k_resolve = nullptr;
+    // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
+    bool debug_stats = false;
+    uint32_t work_flags = 0;
+    void* d_debug = nullptr;
     // scene
     int32_t nspheres = 0;
-    float4* d_geom = nullptr;
+    float4* d_geom = nullptr;  // pair-SoA groups of four (+1 padding group)
+    float4* d_center_radius = nullptr;
     float4* d_shade = nullptr;
-    float2* d_rt = nullptr;
+    float* d_material = nullptr;
+    // work decomposition
+    int32_t chunk = 1, nchunks = 1;
+    uint32_t total_pixels = 0, total_items = 0;
+    float4* d_partial = nullptr;  // [nchunks][total_pixels] chunk sums
     // per-frame inputs / outputs
     float2* d_jitter = nullptr;
     float4* d_fb_own = nullptr;
@@ -86,11 +98,13 @@ std::string library_dir() {
 
 void free_scene() {
     if (g.d_geom) (void)hipFree(g.d_geom);
+    if (g.d_center_radius) (void)hipFree(g.d_center_radius);
     if (g.d_shade) (void)hipFree(g.d_shade);
-    if (g.d_rt) (void)hipFree(g.d_rt);
+    if (g.d_material) (void)hipFree(g.d_material);
     g.d_geom = nullptr;
+    g.d_center_radius = nullptr;
     g.d_shade = nullptr;
-    g.d_rt = nullptr;
+    g.d_material = nullptr;
     g.nspheres = 0;
 }
 
@@ -100,6 +114,9 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem, m, "vcrt_trace_smem"));
     VCRT_TRY(hipModuleGetFunction(&g.k_assemble, m, "vcrt_assemble"));
     VCRT_TRY(hipModuleGetFunction(&g.k_fill, m, "vcrt_fill"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_resolve, m, "vcrt_resolve"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_lds_stats, m, "vcrt_trace_lds_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats"));
     return VK_SUCCESS;
 }
 
@@ -128,7 +145,7 @@ bool desc_valid(const vcrt_render_desc& d) {
         return false;
     if (static_cast<int64_t>(d.width) * d.height > (int64_t{1} << 31)) return false;
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
-    if (d.stripe_height < 0 || d.blocks_per_cu < 0) return false;
+    if (d.stripe_height < 0 || d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
     if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_SMEM) return false;
     return true;
 }
@@ -201,6 +218,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         return fail(r);
     if ((r = to_vk(hipEventCreate(&g.ev_start))) != VK_SUCCESS) return fail(r);
     if ((r = to_vk(hipEventCreate(&g.ev_stop))) != VK_SUCCESS) return fail(r);
+    if ((r = to_vk(hipEventCreate(&g.ev_resolve))) != VK_SUCCESS) return fail(r);
     if ((r = load_code_object(g.desc.code_object_path)) != VK_SUCCESS) return fail(r);
     g.desc.code_object_path = nullptr;  // not owned
 
@@ -231,7 +249,26 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         if ((r = to_vk(hipMemset(g.d_fb_own, 0, g.fb_bytes))) != VK_SUCCESS) return fail(r);
     }
     g.d_fb = g.d_fb_own;
+    // Work decomposition: (8x8 tile, chunk of K samples) items; chunk sums in a slab.
+    g.total_pixels = static_cast<uint32_t>(g.local_rows) * static_cast<uint32_t>(g.desc.width);
+    g.chunk = g.desc.accumulate_chunk > 0 ? g.desc.accumulate_chunk : kDefaultChunk;
+    if (g.chunk > spp) g.chunk = spp;
+    g.nchunks = (spp + g.chunk - 1) / g.chunk;
+    {
+        const uint64_t tiles = (static_cast<uint64_t>(g.total_pixels) + 63) / 64;
+        const uint64_t items = tiles * 64 * static_cast<uint64_t>(g.nchunks);
+        if (items >= (uint64_t{1} << 31)) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
+        g.total_items = static_cast<uint32_t>(items);
+    }
+    if (g.nchunks > 1 && g.total_pixels) {
+        const size_t slab = sizeof(float4) * g.total_pixels * static_cast<size_t>(g.nchunks);
+        if ((r = to_vk(hipMalloc(&g.d_partial, slab))) != VK_SUCCESS) return fail(r);
+    }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
+    if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VCRT_WORK_ORDER"))
+        if (std::strcmp(e, "reverse") == 0) g.work_flags |= vcrt::kFlagReverseOrder;
+    if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, 64))) != VK_SUCCESS) return fail(r);
 
     // The reference's world[] is compiled in; default to the same final scene.
     std::vector<vcrt_sphere> world;
@@ -239,31 +276,60 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if ((r = vcrt_set_scene(world.data(), static_cast<int32_t>(world.size()))) != VK_SUCCESS)
         return fail(r);
     g.stats.local_rows = g.local_rows;
+    g.stats.accumulate_chunk = g.chunk;
     return VCRT_SUCCESS;
 }
 
 vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (count < 0 || (count > 0 && !spheres)) return VCRT_ERROR_INITIALIZATION_FAILED;
-    std::vector<float4> geom(count), shade(count);
-    std::vector<float2> rt(count);
+    // Scan table: groups of four spheres in pair-SoA form
+    //   (cx0,cx1,cy0,cy1) (cz0,cz1,r0²,r1²) (cx2,cx3,cy2,cy3) (cz2,cz3,r2²,r3²),
+    // r² = radius*radius as hit_sphere computes it (functions.glsl:18). The last group is
+    // padded with far-away empty spheres and one extra group follows for the prefetch; the
+    // kernel never accepts a padding index anyway.
+    const int32_t ngroups = (count + 3) / 4;
+    std::vector<float> table(static_cast<size_t>(ngroups + 1) * 16, 0.0f);
+    for (int32_t j = 0; j < 4 * (ngroups + 1); j++) {
+        float* gq = &table[static_cast<size_t>(j / 4) * 16];
+        const int pair = (j % 4) / 2, e = j % 2;
+        float cx = 0.f, cy = 0.f, cz = 0.f, r2 = -3.0e38f;
+        if (j < count) {
+            const vcrt_sphere& sp = spheres[j];
+            cx = sp.center[0];
+            cy = sp.center[1];
+            cz = sp.center[2];
+            r2 = sp.radius * sp.radius;
+        }
+        float* base = gq + 8 * pair;
+        base[0 + e] = cx;
+        base[2 + e] = cy;
+        base[4 + e] = cz;
+        base[6 + e] = r2;
+    }
+    std::vector<float4> cr(count), shade(count);
+    std::vector<float> mat(count);
     for (int32_t i = 0; i < count; i++) {
-        const vcrt_sphere& s = spheres[i];
-        const float r2 = s.radius * s.radius;  // s.radius*s.radius, functions.glsl:18
-        geom[i] = make_float4(s.center[0], s.center[1], s.center[2], r2);
-        shade[i] = make_float4(s.colour[0], s.colour[1], s.colour[2], s.texture[1]);
-        rt[i] = make_float2(s.radius, s.texture[0]);
+        const vcrt_sphere& sp = spheres[i];
+        cr[i] = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
+        shade[i] = make_float4(sp.colour[0], sp.colour[1], sp.colour[2], sp.texture[1]);
+        mat[i] = sp.texture[0];
     }
     (void)hipStreamSynchronize(g.stream);
     free_scene();
+    VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float) * table.size()));
+    VCRT_TRY(hipMemcpy(g.d_geom, table.data(), sizeof(float) * table.size(),
+                       hipMemcpyHostToDevice));
     if (count > 0) {
-        VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float4) * count));
+        VCRT_TRY(hipMalloc(&g.d_center_radius, sizeof(float4) * count));
         VCRT_TRY(hipMalloc(&g.d_shade, sizeof(float4) * count));
-        VCRT_TRY(hipMalloc(&g.d_rt, sizeof(float2) * count));
-        VCRT_TRY(hipMemcpy(g.d_geom, geom.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
+        VCRT_TRY(hipMalloc(&g.d_material, sizeof(float) * count));
+        VCRT_TRY(hipMemcpy(g.d_center_radius, cr.data(), sizeof(float4) * count,
+                           hipMemcpyHostToDevice));
         VCRT_TRY(
             hipMemcpy(g.d_shade, shade.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
-        VCRT_TRY(hipMemcpy(g.d_rt, rt.data(), sizeof(float2) * count, hipMemcpyHostToDevice));
+        VCRT_TRY(
+            hipMemcpy(g.d_material, mat.data(), sizeof(float) * count, hipMemcpyHostToDevice));
     }
     g.nspheres = count;
     g.stats.nspheres = count;
@@ -273,26 +339,30 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
 vcrt_result vcrt_draw_next_frame(void) {
     if (!g.begun || !g.stage.module) return VCRT_ERROR_INITIALIZATION_FAILED;
     const auto t0 = std::chrono::steady_clock::now();
-    const uint32_t items = static_cast<uint32_t>(g.local_rows) * g.desc.width;
+    const uint32_t pixels = g.total_pixels;
     g.stats.segments = 0;
     g.stats.kernel_ms = 0.0;
-    if (items != 0 && g.desc.max_depth == 0) {
+    g.stats.resolve_ms = 0.0;
+    if (pixels != 0 && g.desc.max_depth == 0) {
         // ray_color with MAX_RECURSION_LEVEL 0 returns its undefined value (canonical 0) for
         // every sample without scanning: the frame is (0,0,0,1).
-        vcrt::FillParams fp{g.d_fb, items, make_float4(0.f, 0.f, 0.f, 1.f)};
-        const uint32_t grid = std::min<uint32_t>((items + 255) / 256, 4096);
+        vcrt::FillParams fp{g.d_fb, pixels, make_float4(0.f, 0.f, 0.f, 1.f)};
+        const uint32_t grid = std::min<uint32_t>((pixels + 255) / 256, 4096);
         VkResult r = launch(g.k_fill, grid, 256, 0, fp);
         if (r != VK_SUCCESS) return r;
     }
-    if (items != 0 && g.desc.max_depth > 0) {
+    if (pixels != 0 && g.desc.max_depth > 0) {
         vcrt::TraceParams p{};
         p.geom = g.d_geom;
+        p.center_radius = g.d_center_radius;
         p.shade = g.d_shade;
-        p.rt = g.d_rt;
+        p.material = g.d_material;
         p.jitter = g.d_jitter;
         p.out = g.d_fb;
+        p.partial = g.d_partial;
         p.work = static_cast<uint32_t*>(g.d_counters);
         p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
+        p.debug = static_cast<unsigned long long*>(g.d_debug);
         p.nspheres = g.nspheres;
         p.width = g.desc.width;
         p.height = g.desc.height;
@@ -302,19 +372,26 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.world = g.desc.world_size;
         p.stripe_h = g.desc.stripe_height;
         p.local_rows = g.local_rows;
-        p.total_items = items;
+        p.total_pixels = pixels;
+        p.total_items = g.total_items;
+        p.chunk = g.chunk;
+        p.nchunks = g.nchunks;
+        p.flags = g.work_flags;
         const vcrt::f3 v[4] = {g.cam.pixel00, g.cam.delta_u, g.cam.delta_v, g.cam.center};
         for (int i = 0; i < 4; i++) {
             p.cam[3 * i + 0] = v[i].x;
             p.cam[3 * i + 1] = v[i].y;
             p.cam[3 * i + 2] = v[i].z;
         }
-        const uint32_t geom_lds = static_cast<uint32_t>(sizeof(float4) * g.nspheres);
+        // scan table: (groups + 1 padding group) x 64 B
+        const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
         int variant = g.desc.kernel_variant;
         if (variant == VCRT_KERNEL_AUTO)
             variant = geom_lds <= 40 * 1024 ? VCRT_KERNEL_LDS : VCRT_KERNEL_SMEM;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
         hipFunction_t f = variant == VCRT_KERNEL_LDS ? g.k_trace_lds : g.k_trace_smem;
+        if (g.debug_stats)
+            f = variant == VCRT_KERNEL_LDS ? g.k_trace_lds_stats : g.k_trace_smem_stats;
         const uint32_t lds = variant == VCRT_KERNEL_LDS ? geom_lds : 0;
         const uint32_t block = 256;
         int per_cu = g.desc.blocks_per_cu;
@@ -327,10 +404,23 @@ vcrt_result vcrt_draw_next_frame(void) {
         }
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
         VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
+        if (g.debug_stats) {
+            unsigned long long init[8] = {0, 0, 0, 0, 0, ~0ull, 0, 0};
+            VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
+                                    g.stream));
+        }
         VCRT_TRY(hipEventRecord(g.ev_start, g.stream));
         VkResult r = launch(f, grid, block, lds, p);
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
+        if (g.nchunks > 1) {
+            vcrt::ResolveParams rp{g.d_partial, g.d_fb, pixels, g.nchunks,
+                                   g.desc.samples_per_pixel, g.desc.width, g.local_rows};
+            const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
+            r = launch(g.k_resolve, rgrid, 256, 0, rp);
+            if (r != VK_SUCCESS) return r;
+            VCRT_TRY(hipEventRecord(g.ev_resolve, g.stream));
+        }
         unsigned long long counters[2] = {0, 0};
         VCRT_TRY(hipMemcpyAsync(counters, g.d_counters, sizeof(counters), hipMemcpyDeviceToHost,
                                 g.stream));
@@ -338,7 +428,14 @@ vcrt_result vcrt_draw_next_frame(void) {
         float ms = 0.f;
         VCRT_TRY(hipEventElapsedTime(&ms, g.ev_start, g.ev_stop));
         g.stats.kernel_ms = ms;
+        if (g.nchunks > 1) {
+            VCRT_TRY(hipEventElapsedTime(&ms, g.ev_stop, g.ev_resolve));
+            g.stats.resolve_ms = ms;
+        }
         g.stats.segments = counters[1];
+        if (g.debug_stats)
+            VCRT_TRY(hipMemcpy(g.stats.debug, g.d_debug, sizeof(g.stats.debug),
+                               hipMemcpyDeviceToHost));
         g.stats.grid_blocks = static_cast<int32_t>(grid);
         g.stats.block_threads = static_cast<int32_t>(block);
         g.stats.kernel_variant = variant;
@@ -347,7 +444,7 @@ vcrt_result vcrt_draw_next_frame(void) {
     VCRT_TRY(hipStreamSynchronize(g.stream));
     g.stats.sphere_tests = g.stats.segments * static_cast<uint64_t>(g.nspheres);
     g.stats.samples =
-        static_cast<uint64_t>(items) * static_cast<uint64_t>(g.desc.samples_per_pixel);
+        static_cast<uint64_t>(pixels) * static_cast<uint64_t>(g.desc.samples_per_pixel);
     g.stats.frames += 1;
     g.stats.frame_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -361,9 +458,12 @@ vcrt_result vcrt_end(void) {
     if (g.d_jitter) (void)hipFree(g.d_jitter);
     if (g.d_fb_own) (void)hipFree(g.d_fb_own);
     if (g.d_counters) (void)hipFree(g.d_counters);
+    if (g.d_debug) (void)hipFree(g.d_debug);
     DestroyShaderStage(&g.stage);
     if (g.ev_start) (void)hipEventDestroy(g.ev_start);
     if (g.ev_stop) (void)hipEventDestroy(g.ev_stop);
+    if (g.ev_resolve) (void)hipEventDestroy(g.ev_resolve);
+    if (g.d_partial) (void)hipFree(g.d_partial);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = RendererState{};
     return VCRT_SUCCESS;

@@ -2,22 +2,25 @@
 // Lambertian / metal / glass scatter -> multi-bounce radiance accumulation, written for
 // gfx950 (CDNA4, wave64) as a persistent-lanes wavefront tracer.
 //
-// Reference semantics (quirks kept, see DESIGN.md Appendix):
+// Reference semantics (quirks kept, see DESIGN.md appendix):
 //   shaders/shader.comp:16-58            camera ray per sample, accumulate, divide, store
 //   shaders/include/functions.glsl:14-40 hit_sphere (strict <, index-order tie break)
 //   shaders/include/functions.glsl:65-92 ray_color bounce loop, sky on miss
 //   shaders/include/textures.glsl:19-71  lambertian / metal / glass scatter
 //
 // MI355X design:
-//   * One pixel per lane, all of its samples in sample order (so the fp32 sum is the
-//     reference's sequential sum, bit for bit). A lane whose path ends starts its next
-//     sample at once (path regeneration) and a lane whose pixel is done takes the next pixel
-//     from a wave-aggregated atomic work counter, so lanes stay busy until the queue drains.
-//   * Ray state lives in VGPRs. The sphere list (center, r^2) is staged once per workgroup in
-//     LDS (kLds) or read through the scalar cache with wave-uniform s_load (!kLds); either way
-//     every lane tests sphere j at the same time, so the data is a broadcast.
-//   * Only fp32 add/sub/mul plus correctly rounded div/sqrt, no contraction: the results are
-//     bit-identical to the CPU oracle. No MFMA (branchy scalar math, not a contraction).
+//   * Work items are (8x8 pixel tile, chunk of K samples): one lane per pixel, the chunk's
+//     samples in order. A lane whose path ends starts its next sample at once (path
+//     regeneration); a lane whose chunk is done takes the next item from a wave-aggregated
+//     atomic counter. Chunk sums go to a [chunk][pixel] scratch slab in HBM and vcrt_resolve
+//     adds them in chunk order (K >= spp: no slab, the reference's sequential sum).
+//   * Ray state lives in VGPRs. The sphere list is stored as pair-SoA groups of four
+//     (cx0 cx1 cy0 cy1 | cz0 cz1 r0^2 r1^2 | ...) and tested two spheres per packed-fp32
+//     instruction (v_pk_add_f32 / v_pk_mul_f32: 2 lane-ops per issue, the only way gfx950
+//     reaches its fp32 peak). Staged once per workgroup in LDS (kLds) or read with
+//     wave-uniform scalar loads (!kLds); all lanes test the same spheres at the same time.
+//   * Only fp32 add/sub/mul plus correctly rounded div/sqrt, no contraction: results are
+//     bit-identical to the CPU oracle for the same accumulation order. No MFMA.
 #include <hip/hip_runtime.h>
 
 #include "vcrt_kernel_abi.h"
@@ -29,7 +32,7 @@ using namespace vcrt;
 
 namespace {
 
-constexpr int kBand = 8;  // rows per work band (8x8 tiles of 64 consecutive items)
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -38,20 +41,115 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
 
 typedef __attribute__((address_space(4))) const float4 cfloat4;
 
+// One group = four spheres in pair-SoA form: q[0] = (cx0,cx1,cy0,cy1), q[1] = (cz0,cz1,r0²,r1²),
+// q[2] = (cx2,cx3,cy2,cy3), q[3] = (cz2,cz3,r2²,r3²).
+struct Group {
+    float4 q[4];
+};
+
 template <bool kLds>
-__device__ __forceinline__ float4 sphere_geom(const float4* lds, const TraceParams& p, int j) {
+__device__ __forceinline__ Group load_group(const float4* lds, const TraceParams& p, int gi) {
+    Group g;
     if constexpr (kLds) {
-        return lds[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g.q[k] = lds[4 * gi + k];
     } else {
-        return ((cfloat4*)p.geom)[j];  // uniform index -> s_load through the scalar cache
+        cfloat4* s = (cfloat4*)p.geom;  // wave-uniform index -> s_load through the scalar cache
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g.q[k] = s[4 * gi + k];
+    }
+    return g;
+}
+
+// hit_sphere (functions.glsl:14-40) after the discriminant test passed: nearest root in
+// (min_t, max_t), strict comparisons, max_t shrinks on acceptance.
+__device__ __forceinline__ void accept_root(float hb, float disc, float a, float& max_t, int& best,
+                                            int j) {
+    const float min_t = 0.001f;
+    const float sq = __builtin_sqrtf(disc);
+    float root = (-hb - sq) / a;
+    bool ok = true;
+    if (root <= min_t || max_t <= root) {
+        root = (-hb + sq) / a;
+        ok = !(root <= min_t || max_t <= root);
+    }
+    if (ok) {
+        max_t = root;
+        best = j;
     }
 }
 
+// Discriminants of two spheres at once (hit_sphere's first half, element-wise exact):
+// oc = o - c; half_b = dot(oc, d); c = dot(oc, oc) - r²; disc = half_b² - a·c.
+__device__ __forceinline__ void pair_disc(const v2f ox, const v2f oy, const v2f oz, const v2f dx,
+                                          const v2f dy, const v2f dz, const v2f a2, float4 xy,
+                                          float4 zr, v2f& hb, v2f& disc) {
+    const v2f cx = {xy.x, xy.y}, cy = {xy.z, xy.w}, cz = {zr.x, zr.y}, r2 = {zr.z, zr.w};
+    const v2f ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    hb = ocx * dx + ocy * dy + ocz * dz;
+    const v2f cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
+    disc = hb * hb - a2 * cc;
+}
+
+// The sphere-list scan of one ray segment (functions.glsl:77-81): four spheres per step as two
+// packed pairs, the next group prefetched, one wave-uniform branch into the rare root path,
+// which then visits the four candidates in index order so ties resolve to the earlier sphere.
 template <bool kLds>
+__device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4* lds, int n,
+                                             const f3 o, const f3 d, float& max_t, int& best,
+                                             uint32_t& hit_groups) {
+    const float a = dot(d, d);  // loop-invariant in hit_sphere: hoisting is exact
+    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
+    const int ngroups = (n + 3) >> 2;
+    Group g = load_group<kLds>(lds, p, 0);
+    for (int gi = 0; gi < ngroups; ++gi) {
+        const Group nx = load_group<kLds>(lds, p, gi + 1);  // table padded by one group
+        v2f hb01, d01, hb23, d23;
+        pair_disc(ox, oy, oz, dx, dy, dz, a2, g.q[0], g.q[1], hb01, d01);
+        pair_disc(ox, oy, oz, dx, dy, dz, a2, g.q[2], g.q[3], hb23, d23);
+        const bool h0 = !(d01.x < 0.0f), h1 = !(d01.y < 0.0f), h2 = !(d23.x < 0.0f),
+                   h3 = !(d23.y < 0.0f);
+        if (__ballot(h0) | __ballot(h1) | __ballot(h2) | __ballot(h3)) {
+            ++hit_groups;
+            const int j = 4 * gi;  // padding spheres (index >= n) are never accepted
+            if (h0) accept_root(hb01.x, d01.x, a, max_t, best, j + 0);
+            if (h1 && j + 1 < n) accept_root(hb01.y, d01.y, a, max_t, best, j + 1);
+            if (h2 && j + 2 < n) accept_root(hb23.x, d23.x, a, max_t, best, j + 2);
+            if (h3 && j + 3 < n) accept_root(hb23.y, d23.y, a, max_t, best, j + 3);
+        }
+        g = nx;
+    }
+}
+
+// Work item -> pixel. Pixels are numbered q = 0..total-1 in 8-row bands, eight rows of one
+// column per 8 consecutive q, so 64 consecutive q form an 8x8 tile; local row lr maps to the
+// global row of this rank's interleaved stripes.
+struct Pixel {
+    uint32_t x, y, lr;
+};
+
+__device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t local_rows,
+                                          uint32_t stripe_h, uint32_t world, uint32_t rank) {
+    const uint32_t band = q / (8u * W);
+    const uint32_t r = q - band * 8u * W;
+    const uint32_t rows_left = local_rows - band * 8u;
+    const uint32_t rows_in_band = rows_left < 8u ? rows_left : 8u;
+    Pixel px;
+    px.x = r / rows_in_band;
+    px.lr = band * 8u + (r - px.x * rows_in_band);
+    const uint32_t ls = px.lr / stripe_h;
+    const uint32_t within = px.lr - ls * stripe_h;
+    px.y = (ls * world + rank) * stripe_h + within;
+    return px;
+}
+
+template <bool kLds, bool kStats>
 __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geom) {
     const int n = p.nspheres;
     if constexpr (kLds) {
-        for (int i = threadIdx.x; i < n; i += blockDim.x) lds_geom[i] = p.geom[i];
+        const int nq = 4 * (((n + 3) >> 2) + 1);
+        for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = p.geom[i];
         __syncthreads();
     }
     const uint32_t lane = threadIdx.x & 63u;
@@ -60,122 +158,85 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     const f3 dv = mk(p.cam[6], p.cam[7], p.cam[8]);
     const f3 cam = mk(p.cam[9], p.cam[10], p.cam[11]);
     const float spp_f = (float)p.spp;
-    const uint32_t W = (uint32_t)p.width;
-    const float min_t = 0.001f;
+    const uint32_t nchunks = (uint32_t)p.nchunks;
+    const bool reverse = (p.flags & kFlagReverseOrder) != 0;
 
     bool done = false, need = true;
-    int sample = 0, pass = 0;
-    uint32_t out_index = 0;
+    int sample = 0, sample_end = 0, pass = 0;
+    uint32_t q = 0, chunk = 0, out_index = 0;
     f3 pc = mk(0.f, 0.f, 0.f), o = pc, d = pc, atten = pc, acc = pc;
     unsigned long long segs = 0;
+    uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
 
     for (;;) {
-        // ---- take new pixels for lanes that finished theirs (one atomic per wave) ----
-        const uint64_t need_mask = __ballot(need && !done);
-        if (need_mask) {
+        // ---- lanes whose item is finished take the next ones (one atomic per wave) ----
+        uint64_t need_mask = __ballot(need && !done);
+        while (need_mask) {
+            if constexpr (kStats) ++st_fetch;
             const int leader = __ffsll((unsigned long long)need_mask) - 1;
             uint32_t base = 0;
             if ((int)lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need_mask));
             base = __shfl(base, leader);
             if (need && !done) {
-                const uint32_t item = base + lanes_below(need_mask);
+                uint32_t item = base + lanes_below(need_mask);
                 if (item >= p.total_items) {
                     done = true;
                 } else {
-                    const uint32_t band = item / (kBand * W);
-                    const uint32_t r = item - band * kBand * W;
-                    const uint32_t rows_left = (uint32_t)p.local_rows - band * kBand;
-                    const uint32_t rows_in_band = rows_left < kBand ? rows_left : kBand;
-                    const uint32_t x = r / rows_in_band;
-                    const uint32_t lr = band * kBand + (r - x * rows_in_band);
-                    const uint32_t ls = lr / (uint32_t)p.stripe_h;
-                    const uint32_t within = lr - ls * (uint32_t)p.stripe_h;
-                    const uint32_t y =
-                        (ls * (uint32_t)p.world + (uint32_t)p.rank) * (uint32_t)p.stripe_h + within;
-                    out_index = lr * W + x;
-                    // shader.comp:43  pixel00 + x*delta_u + y*delta_v
-                    pc = add(add(p00, scale((float)x, du)), scale((float)y, dv));
-                    acc = mk(0.f, 0.f, 0.f);
-                    sample = 0;
-                    // first camera ray, shader.comp:48-52
-                    const float2 jt = p.jitter[0];
-                    const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
-                    o = cam;
-                    d = sub(ps, cam);
-                    atten = mk(1.f, 1.f, 1.f);
-                    pass = 0;
+                    if (reverse) item = p.total_items - 1u - item;
+                    // item = (tile, chunk, slot): 64 consecutive items = one tile x one chunk
+                    const uint32_t tile_chunk = item >> 6;
+                    const uint32_t tile = tile_chunk / nchunks;
+                    chunk = tile_chunk - tile * nchunks;
+                    q = tile * 64u + (item & 63u);
+                    if (q < p.total_pixels) {  // the last tile may be partial
+                        const Pixel px =
+                            pixel_of(q, (uint32_t)p.width, (uint32_t)p.local_rows,
+                                     (uint32_t)p.stripe_h, (uint32_t)p.world, (uint32_t)p.rank);
+                        out_index = px.lr * (uint32_t)p.width + px.x;
+                        // shader.comp:43  pixel00 + x*delta_u + y*delta_v
+                        pc = add(add(p00, scale((float)px.x, du)), scale((float)px.y, dv));
+                        acc = mk(0.f, 0.f, 0.f);
+                        sample = (int)(chunk * (uint32_t)p.chunk);
+                        sample_end = min(sample + p.chunk, p.spp);
+                        // first camera ray of the chunk, shader.comp:48-52
+                        const float2 jt = p.jitter[sample];
+                        const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
+                        o = cam;
+                        d = sub(ps, cam);
+                        atten = mk(1.f, 1.f, 1.f);
+                        pass = 0;
+                        need = false;
+                    }
                 }
-                need = false;
             }
+            need_mask = __ballot(need && !done);  // lanes that drew an empty slot retry
         }
-        if (__ballot(!done) == 0) break;
+        const uint64_t live = __ballot(!done);
+        if (live == 0) break;
+        if constexpr (kStats) {
+            ++st_iters;
+            st_active += (uint64_t)__popcll(live);
+        }
         if (done) continue;
 
         // ---- one segment: scan the whole sphere list (functions.glsl:73-81) ----
         ++segs;
-        const float a = dot(d, d);  // loop-invariant in hit_sphere: hoisting is exact
         float max_t = 1e5f;
         int best = -1;
-        int j = 0;
-        const int n4 = n & ~3;
-        for (; j < n4; j += 4) {
-            float hb[4], disc[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 g = sphere_geom<kLds>(lds_geom, p, j + k);
-                const float ocx = o.x - g.x, ocy = o.y - g.y, ocz = o.z - g.z;
-                hb[k] = ocx * d.x + ocy * d.y + ocz * d.z;
-                const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - g.w;
-                disc[k] = hb[k] * hb[k] - a * cc;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!(disc[k] < 0.0f)) {
-                    const float sq = __builtin_sqrtf(disc[k]);
-                    float root = (-hb[k] - sq) / a;
-                    bool ok = true;
-                    if (root <= min_t || max_t <= root) {
-                        root = (-hb[k] + sq) / a;
-                        ok = !(root <= min_t || max_t <= root);
-                    }
-                    if (ok) {
-                        max_t = root;
-                        best = j + k;
-                    }
-                }
-            }
-        }
-        for (; j < n; ++j) {
-            const float4 g = sphere_geom<kLds>(lds_geom, p, j);
-            const float ocx = o.x - g.x, ocy = o.y - g.y, ocz = o.z - g.z;
-            const float hb = ocx * d.x + ocy * d.y + ocz * d.z;
-            const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - g.w;
-            const float disc = hb * hb - a * cc;
-            if (!(disc < 0.0f)) {
-                const float sq = __builtin_sqrtf(disc);
-                float root = (-hb - sq) / a;
-                bool ok = true;
-                if (root <= min_t || max_t <= root) {
-                    root = (-hb + sq) / a;
-                    ok = !(root <= min_t || max_t <= root);
-                }
-                if (ok) {
-                    max_t = root;
-                    best = j;
-                }
-            }
-        }
+        uint32_t hit_groups = 0;
+        scan_spheres<kLds>(p, lds_geom, n, o, d, max_t, best, hit_groups);
+        if constexpr (kStats) st_hitgroups += hit_groups;
 
         // ---- shade (textures.glsl) or sky (functions.glsl:85-89) ----
         bool ended = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
         if (best >= 0) {
-            const float4 g = p.geom[best];
-            const float2 rt = p.rt[best];
+            const float4 cr = p.center_radius[best];
             const float4 sh = p.shade[best];
+            const float mat = p.material[best];
             const f3 point = add(scale(max_t, d), o);
-            const f3 normal = divs(sub(point, mk(g.x, g.y, g.z)), rt.x);
-            const int type = (int)rt.y;
+            const f3 normal = divs(sub(point, mk(cr.x, cr.y, cr.z)), cr.w);
+            const int type = (int)mat;
             const f3 albedo = mk(sh.x, sh.y, sh.z);
             const float param = sh.w;
             // first rand: rand(dir.xy) for lambertian/metal, rand(point.xy) for glass
@@ -231,8 +292,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         if (ended) {
             acc = add(acc, contrib);
             ++sample;
-            if (sample == p.spp) {
-                p.out[out_index] = make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
+            if (sample == sample_end) {
+                if (nchunks == 1u)
+                    p.out[out_index] =
+                        make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
+                else
+                    p.partial[(size_t)chunk * p.total_pixels + q] =
+                        make_float4(acc.x, acc.y, acc.z, 0.0f);
                 need = true;
             } else {
                 const float2 jt = p.jitter[sample];
@@ -250,20 +316,61 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
     if (lane == 0 && total) atomicAdd(p.segments, total);
+    if constexpr (kStats) {
+        if (lane == 0 && p.debug) {
+            atomicAdd(p.debug + 0, (unsigned long long)st_iters);
+            atomicAdd(p.debug + 1, (unsigned long long)st_active);
+            atomicAdd(p.debug + 2, (unsigned long long)st_hitgroups);
+            atomicAdd(p.debug + 3, (unsigned long long)st_fetch);
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            atomicMax(p.debug + 4, t);
+            atomicMin(p.debug + 5, t);
+            atomicAdd(p.debug + 6, t >> 8);  // mean wave end time (in 256-tick units)
+            atomicAdd(p.debug + 7, 1ull);
+        }
+    }
 }
 
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_lds(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_geom[];
-    trace_impl<true>(p, lds_geom);
+    trace_impl<true, false>(p, lds_geom);
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem(TraceParams p) {
-    trace_impl<false>(p, nullptr);
+    trace_impl<false, false>(p, nullptr);
 }
 
-// Reassemble the rank-interleaved 16-row stripes gathered from every rank into one frame.
+// Diagnostics builds (VCRT_DEBUG_STATS=1): same kernels plus lane-occupancy/tail counters.
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_lds_stats(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_geom[];
+    trace_impl<true, true>(p, lds_geom);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem_stats(TraceParams p) {
+    trace_impl<false, true>(p, nullptr);
+}
+
+// Chunk sums -> pixels in chunk order: ((P0 + P1) + P2) + ..., then / spp (shader.comp:56).
+extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) {
+    const float spp_f = (float)p.spp;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.total_pixels;
+         q += gridDim.x * blockDim.x) {
+        float4 s = p.partial[q];
+        for (int c = 1; c < p.nchunks; ++c) {
+            const float4 v = p.partial[(size_t)c * p.total_pixels + q];
+            s.x = s.x + v.x;
+            s.y = s.y + v.y;
+            s.z = s.z + v.z;
+        }
+        const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.local_rows, 1u, 1u, 0u);
+        p.out[px.lr * (uint32_t)p.width + px.x] =
+            make_float4(s.x / spp_f, s.y / spp_f, s.z / spp_f, 1.0f);
+    }
+}
+
+// Reassemble the rank-interleaved stripes gathered from every rank into one frame.
 extern "C" __global__ __launch_bounds__(256) void vcrt_assemble(AssembleParams p) {
     const uint32_t total = (uint32_t)p.width * (uint32_t)p.height;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;

@@ -13,21 +13,38 @@
 
 namespace vcrt {
 
-// Work items are the rank's pixels in 8-row bands, 8 rows x 1 column per 8 consecutive
-// items, so 64 consecutive items form an 8x8 tile (see item_to_pixel in tracer.hip).
+// Work items are (8x8 tile, sample chunk, lane slot): 64 consecutive items are one tile of
+// pixels at one chunk of samples (see tracer.hip). Pixels q = 0..total_pixels-1 are numbered
+// in 8-row bands with eight rows of one column per 8 consecutive q.
 struct TraceParams {
-    const float4* geom;   // [n] (center.xyz, radius*radius)      -- hot: read every segment
-    const float4* shade;  // [n] (colour.rgb, texture.y = param)  -- read once per hit
-    const float2* rt;     // [n] (radius, texture.x = material id)
-    const float2* jitter; // [spp] (-0.5+rand(i,i), -0.5+rand(i+1,i+1)), shader.comp:48
-    float4* out;          // [local_rows * width] rank-local framebuffer, rgba32f
-    uint32_t* work;       // pixel work counter, zeroed before every launch
+    const float4* geom;           // pair-SoA sphere groups (+1 padding group), scan input
+    const float4* center_radius;  // [n] (center.xyz, radius)           -- read once per hit
+    const float4* shade;          // [n] (colour.rgb, texture.y = param)
+    const float* material;        // [n] texture.x = material id
+    const float2* jitter;  // [spp] (-0.5+rand(i,i), -0.5+rand(i+1,i+1)), shader.comp:48
+    float4* out;           // [local_rows * width] rank-local framebuffer, rgba32f
+    float4* partial;       // [nchunks][total_pixels] chunk sums (nchunks > 1)
+    uint32_t* work;        // work-item counter, zeroed before every launch
     unsigned long long* segments;  // ray segments traced, zeroed before every launch
+    unsigned long long* debug;     // diagnostics counters (stats kernels only), may be null
     int32_t nspheres;
     int32_t width, height, spp, max_depth;
     int32_t rank, world, stripe_h, local_rows;
-    uint32_t total_items;  // local_rows * width
-    float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
+    uint32_t total_pixels;  // local_rows * width
+    uint32_t total_items;   // ceil(total_pixels / 64) * 64 * nchunks
+    int32_t chunk;          // samples per work item
+    int32_t nchunks;        // ceil(spp / chunk)
+    uint32_t flags;         // kFlag*
+    float cam[12];          // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
+};
+
+constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
+
+struct ResolveParams {
+    const float4* partial;  // [nchunks][total_pixels]
+    float4* out;            // [local_rows * width]
+    uint32_t total_pixels;
+    int32_t nchunks, spp, width, local_rows;
 };
 
 struct AssembleParams {

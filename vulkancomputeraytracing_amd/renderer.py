@@ -33,6 +33,7 @@ class RenderDesc:
     stripe_height: int = 16
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
+    accumulate_chunk: int = 0       # 0 = 32; >= spp: the reference's sequential order
     code_object_path: str | None = None
     _path_keepalive: bytes | None = field(default=None, repr=False)
 
@@ -50,10 +51,20 @@ class RenderDesc:
         d.stripe_height = self.stripe_height
         d.kernel_variant = self.kernel_variant
         d.blocks_per_cu = self.blocks_per_cu
+        d.accumulate_chunk = self.accumulate_chunk
         if self.code_object_path:
             self._path_keepalive = self.code_object_path.encode()
             d.code_object_path = self._path_keepalive
         return d
+
+
+DEFAULT_ACCUMULATE_CHUNK = 32
+
+
+def effective_chunk(spp: int, accumulate_chunk: int = 0) -> int:
+    """Samples per work item the renderer uses (the oracle's `chunk` for the same order)."""
+    k = accumulate_chunk if accumulate_chunk > 0 else DEFAULT_ACCUMULATE_CHUNK
+    return min(k, spp)
 
 
 def rows_for_rank(height: int, stripe: int, world: int, rank: int) -> list[int]:
@@ -168,7 +179,9 @@ class Renderer:
     def stats(self) -> dict:
         s = N.vcrt_stats()
         N.check("vcrt_get_stats", self._lib.vcrt_get_stats(ctypes.byref(s)))
-        return {name: getattr(s, name) for name, _ in N.vcrt_stats._fields_}
+        out = {name: getattr(s, name) for name, _ in N.vcrt_stats._fields_}
+        out["debug"] = list(s.debug)
+        return out
 
 
 def render(desc: RenderDesc, scene="final", frames: int = 1) -> tuple[np.ndarray, dict]:
