@@ -68,7 +68,8 @@ typedef struct vcrt_camera { /* globals.glsl:21-24 */
     float vfov; /* degrees */
 } vcrt_camera;
 
-/* Kernel variants. AUTO picks LDS staging when the sphere list fits, scalar cache otherwise. */
+/* Kernel variants. AUTO: scalar-cache (SMEM) sphere reads while the scan table fits the
+ * scalar cache (<= 16 KB, ~1000 spheres), LDS staging above that. */
 #define VCRT_KERNEL_AUTO 0
 #define VCRT_KERNEL_LDS 1
 #define VCRT_KERNEL_SMEM 2
@@ -85,7 +86,7 @@ typedef struct vcrt_render_desc {
     int32_t stripe_height; /* rows per interleaved stripe; 0 = 16 */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
-    int32_t accumulate_chunk; /* samples per work item (0 = 32). A pixel's samples are summed
+    int32_t accumulate_chunk; /* samples per work item (0 = 16). A pixel's samples are summed
                                  in order within a chunk and the chunk sums in chunk order;
                                  >= samples_per_pixel reproduces the reference's sequential
                                  sum (shader.comp:46-54) exactly. */

@@ -68,7 +68,7 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
 @pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
 @pytest.mark.parametrize("scene,w,h,spp,depth,chunk", [
     ("final", 64, 36, 64, 10, 16),   # 4 chunks
-    ("final", 48, 30, 40, 10, 0),    # default chunk 32: chunks of 32 + 8 (ragged)
+    ("final", 48, 30, 40, 10, 0),    # default chunk 16: chunks of 16 + 16 + 8 (ragged)
     ("three", 72, 40, 96, 8, 7),     # 14 chunks, last one of 5
     ("final", 40, 24, 33, 10, 33),   # one chunk = the reference's sequential order
 ])

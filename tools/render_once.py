@@ -21,11 +21,12 @@ def main():
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--frames", type=int, default=1)
     p.add_argument("--code-object", default=None)
+    p.add_argument("--chunk", type=int, default=0)
     a = p.parse_args()
     desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
                          max_depth=a.depth, kernel_variant=a.variant,
                          blocks_per_cu=a.blocks_per_cu, device=0,
-                         code_object_path=a.code_object)
+                         code_object_path=a.code_object, accumulate_chunk=a.chunk)
     with vc.Renderer(desc, a.scene) as r:
         out = []
         for _ in range(a.frames):

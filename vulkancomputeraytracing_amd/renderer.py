@@ -33,7 +33,7 @@ class RenderDesc:
     stripe_height: int = 16
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
-    accumulate_chunk: int = 0       # 0 = 32; >= spp: the reference's sequential order
+    accumulate_chunk: int = 0       # 0 = 16; >= spp: the reference's sequential order
     code_object_path: str | None = None
     _path_keepalive: bytes | None = field(default=None, repr=False)
 
@@ -58,7 +58,7 @@ class RenderDesc:
         return d
 
 
-DEFAULT_ACCUMULATE_CHUNK = 32
+DEFAULT_ACCUMULATE_CHUNK = 16
 
 
 def effective_chunk(spp: int, accumulate_chunk: int = 0) -> int:
