@@ -2,8 +2,9 @@
 1920x1080, 1024 spp, max depth 10 (BASELINE.json metric, configs[3]) on N MI355X GPUs.
 
 One step = one DrawNextFrame of the whole frame: on every rank the gfx950 tracer renders the
-rank's interleaved 16-row stripes, then (N > 1) the stripes are all-gathered over RCCL and rank 0
-reassembles the frame. The frame is fixed as N grows (strong scaling).
+rank's interleaved rows (row y belongs to rank y % N), then (N > 1) the rank framebuffers are
+all-gathered over RCCL and rank 0 re-interleaves the frame. The frame is fixed as N grows
+(strong scaling).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
@@ -38,6 +39,8 @@ def parse():
     p.add_argument("--scene", default="final")
     p.add_argument("--variant", type=int, default=0)
     p.add_argument("--blocks-per-cu", type=int, default=0)
+    p.add_argument("--stripe", type=int, default=1)
+    p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU work for the cpu_baseline sample")
@@ -81,6 +84,7 @@ def main():
     import torch.distributed as dist
 
     import vulkancomputeraytracing_amd as vc
+    from vulkancomputeraytracing_amd import distributed as D
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -93,29 +97,26 @@ def main():
 
     desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
                          max_depth=args.depth, device=local_rank, rank=rank, world_size=world,
-                         stripe_height=16, kernel_variant=args.variant,
-                         blocks_per_cu=args.blocks_per_cu)
-    rows_per_rank = max(len(vc.rows_for_rank(args.height, 16, world, r)) for r in range(world))
+                         stripe_height=args.stripe, kernel_variant=args.variant,
+                         blocks_per_cu=args.blocks_per_cu, accumulate_chunk=args.chunk)
+    rows_pad = D.rows_per_rank(args.height, args.stripe, world)
     dev = torch.device("cuda", local_rank)
-    local = torch.zeros((rows_per_rank, args.width, 4), dtype=torch.float32, device=dev)
-    gathered = frame = None
-    if world > 1:
-        gathered = torch.empty((world, rows_per_rank, args.width, 4), dtype=torch.float32,
-                               device=dev)
-        if rank == 0:
-            frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
+    local = torch.zeros((rows_pad, args.width, 4), dtype=torch.float32, device=dev)
+    frame = None
+    if world > 1 and rank == 0:
+        frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
 
     r = vc.Renderer(desc, args.scene)
     r.set_framebuffer_device(local.data_ptr(), local.numel() * 4)
     nspheres = len(vc.builtin_scene(args.scene))
 
     def step():
-        r.draw_next_frame()  # returns when the rank's stripes are complete
+        r.draw_next_frame()  # returns when the rank's rows are complete
         if world > 1:
-            dist.all_gather_into_tensor(gathered, local)
+            gathered = D.gather_stripes(local, rows_pad)
             if rank == 0:
                 torch.cuda.current_stream().synchronize()
-                r.assemble_stripes(gathered.data_ptr(), frame.data_ptr(), rows_per_rank)
+                D.assemble_frame(r, gathered, frame, rows_pad)
 
     for i in range(args.warmup):
         step()
@@ -178,7 +179,8 @@ def main():
                                    f"{args.spp}spp_d{args.depth}",
                        "scene": args.scene, "spheres": nspheres, "width": args.width,
                        "height": args.height, "spp": args.spp, "max_depth": args.depth,
-                       "parallelism": f"stripes16x{world}",
+                       "parallelism": f"row-interleave{args.stripe}x{world}",
+                       "accumulate_chunk": st["accumulate_chunk"],
                        "kernel_variant": st["kernel_variant"],
                        "grid_blocks": st["grid_blocks"]},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),

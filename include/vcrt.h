@@ -83,7 +83,7 @@ typedef struct vcrt_render_desc {
     int32_t device;        /* HIP device ordinal; -1 = current device */
     int32_t rank;          /* this process's shard of the frame */
     int32_t world_size;    /* number of shards (GPUs) */
-    int32_t stripe_height; /* rows per interleaved stripe; 0 = 16 */
+    int32_t stripe_height; /* rows per interleaved stripe; 0 = 1 (row interleave) */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
     int32_t accumulate_chunk; /* samples per work item (0 = 16). A pixel's samples are summed
@@ -111,7 +111,7 @@ typedef struct vcrt_stats {
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
- * (13,2,3)->(0,0,0), vup (0,1,0), vfov 20, rank 0 of 1, stripe 16 (globals.glsl:9-24). */
+ * (13,2,3)->(0,0,0), vup (0,1,0), vfov 20, rank 0 of 1, stripe 1 (globals.glsl:9-24). */
 vcrt_result vcrt_default_desc(vcrt_render_desc* desc);
 
 vcrt_result vcrt_begin(const vcrt_render_desc* desc);

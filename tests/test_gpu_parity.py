@@ -20,7 +20,7 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0, world=1,
-               stripe=16, frames=1, scene_arr=None, chunk=0):
+               stripe=1, frames=1, scene_arr=None, chunk=0):
     desc = vc.RenderDesc(width=width, height=height, samples_per_pixel=spp, max_depth=depth,
                          kernel_variant=variant, rank=rank, world_size=world,
                          stripe_height=stripe, device=0, accumulate_chunk=chunk)
@@ -142,7 +142,7 @@ def test_frames_are_identical(oracle):
     assert_bitwise(a, b, "frame 2 vs frame 1")
 
 
-@pytest.mark.parametrize("world,stripe", [(2, 16), (3, 16), (8, 16), (4, 5)])
+@pytest.mark.parametrize("world,stripe", [(2, 1), (3, 1), (8, 1), (2, 16), (3, 16), (4, 5)])
 def test_sharded_stripes_reassemble_bitwise(world, stripe):
     import torch
     w, h, spp, depth = 72, 90, 2, 10

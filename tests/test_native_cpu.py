@@ -41,7 +41,7 @@ def test_struct_layouts():
     assert d.struct_size == ctypes.sizeof(N.vcrt_render_desc)
     assert (d.width, d.height, d.samples_per_pixel, d.max_depth) == (1280, 720, 1, 50)
     assert list(d.camera.lookfrom) == [13, 2, 3] and d.camera.vfov == 20
-    assert (d.rank, d.world_size, d.stripe_height) == (0, 1, 16)
+    assert (d.rank, d.world_size, d.stripe_height) == (0, 1, 1)
 
 
 def test_product_canonical_math_equals_oracle(oracle):

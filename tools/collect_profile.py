@@ -1,0 +1,54 @@
+"""Collect a gpurun profiling batch (tools/gpu_profile.sh) into profiles/:
+kernel-trace stats of the bench command, PMC summaries, and profiles/traffic.json (HBM bytes per
+launch of the tracer kernel for the bench workload, corrected per MI355X_MICROARCH.md: FETCH_SIZE
+and WRITE_SIZE are KB; gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so it is
+doubled -- an upper bound for the tracer's narrow scalar loads)."""
+import csv
+import collections
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src = os.path.join(ROOT, "gpurun_out", "prof")
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+dst = os.path.join(ROOT, "profiles")
+os.makedirs(dst, exist_ok=True)
+
+
+def pmc(name):
+    path = os.path.join(src, name, "run_counter_collection.csv")
+    agg = collections.defaultdict(float)
+    calls = collections.Counter()
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"].split("(")[0]
+        agg[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+        calls[(k, r["Counter_Name"])] += 1
+    return {f"{k}|{c}": {"sum": v, "dispatches": calls[(k, c)]} for (k, c), v in agg.items()}
+
+
+shutil.copy(os.path.join(src, "kt", "bench_kernel_stats.csv"),
+            os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+bench = json.load(open(os.path.join(src, "kt_bench.json")))
+summary = {"bench_under_rocprof": {k: bench[k] for k in ("value", "ms_per_step", "roofline")}}
+for name in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
+    if os.path.exists(os.path.join(src, name)):
+        summary[name] = pmc(name)
+with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
+    json.dump(summary, f, indent=1)
+
+fetch = summary["pmc_fetch"]["vcrt_trace_smem|FETCH_SIZE"]
+write = summary["pmc_write"]["vcrt_trace_smem|WRITE_SIZE"]
+per_launch = (2 * fetch["sum"] / fetch["dispatches"] + write["sum"] / write["dispatches"]) * 1024
+cfg = bench["config"]
+key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_s{cfg['spp']}_d{cfg['max_depth']}_n1"
+traffic_path = os.path.join(dst, "traffic.json")
+traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
+traffic[key] = {"hbm_bytes_per_launch": per_launch, "fetch_kb": fetch["sum"] / fetch["dispatches"],
+                "write_kb": write["sum"] / write["dispatches"], "round": tag,
+                "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/render_once.py "
+                        "at the bench config; FETCH_SIZE doubled (gfx950 correction)"}
+with open(traffic_path, "w") as f:
+    json.dump(traffic, f, indent=1)
+print(json.dumps(traffic[key]))

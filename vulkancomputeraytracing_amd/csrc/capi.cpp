@@ -178,7 +178,7 @@ vcrt_result vcrt_default_desc(vcrt_render_desc* d) {
     d->device = -1;
     d->rank = 0;
     d->world_size = 1;
-    d->stripe_height = 16;
+    d->stripe_height = 1;  // row interleave: best rank balance (multi-GPU)
     d->kernel_variant = VCRT_KERNEL_AUTO;
     return VCRT_SUCCESS;
 }
@@ -188,7 +188,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (g.begun) vcrt_end();
     g = RendererState{};
     g.desc = *desc;
-    if (g.desc.stripe_height == 0) g.desc.stripe_height = 16;
+    if (g.desc.stripe_height == 0) g.desc.stripe_height = 1;
     g.begun = true;  // from here on vcrt_end() cleans up whatever was created
 
     int count = 0;

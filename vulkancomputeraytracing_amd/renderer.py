@@ -30,7 +30,7 @@ class RenderDesc:
     device: int = -1
     rank: int = 0
     world_size: int = 1
-    stripe_height: int = 16
+    stripe_height: int = 1          # rows per interleaved stripe (1 = row interleave)
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
     accumulate_chunk: int = 0       # 0 = 16; >= spp: the reference's sequential order
