@@ -2,7 +2,7 @@
 1920x1080, 1024 spp, max depth 10 (BASELINE.json metric, configs[3]) on N MI355X GPUs.
 
 One step = one DrawNextFrame of the whole frame: on every rank the gfx950 tracer renders the
-rank's interleaved rows (row y belongs to rank y % N), then (N > 1) the rank framebuffers are
+rank's 8x8 tiles (tile t belongs to rank t % N), then (N > 1) the packed rank framebuffers are
 all-gathered over RCCL and rank 0 re-interleaves the frame. The frame is fixed as N grows
 (strong scaling).
 
@@ -39,7 +39,6 @@ def parse():
     p.add_argument("--scene", default="final")
     p.add_argument("--variant", type=int, default=0)
     p.add_argument("--blocks-per-cu", type=int, default=0)
-    p.add_argument("--stripe", type=int, default=1)
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0,
@@ -97,11 +96,12 @@ def main():
 
     desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
                          max_depth=args.depth, device=local_rank, rank=rank, world_size=world,
-                         stripe_height=args.stripe, kernel_variant=args.variant,
+                         kernel_variant=args.variant,
                          blocks_per_cu=args.blocks_per_cu, accumulate_chunk=args.chunk)
-    rows_pad = D.rows_per_rank(args.height, args.stripe, world)
     dev = torch.device("cuda", local_rank)
-    local = torch.zeros((rows_pad, args.width, 4), dtype=torch.float32, device=dev)
+    tiles_pad = D.tiles_per_rank(args.width, args.height, world)
+    local_elems = args.width * args.height if world == 1 else tiles_pad * 64
+    local = torch.zeros((local_elems, 4), dtype=torch.float32, device=dev)
     frame = None
     if world > 1 and rank == 0:
         frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
@@ -113,10 +113,10 @@ def main():
     def step():
         r.draw_next_frame()  # returns when the rank's rows are complete
         if world > 1:
-            gathered = D.gather_stripes(local, rows_pad)
+            gathered = D.gather_tiles(local, tiles_pad)
             if rank == 0:
                 torch.cuda.current_stream().synchronize()
-                D.assemble_frame(r, gathered, frame, rows_pad)
+                D.assemble_frame(r, gathered, frame, tiles_pad)
 
     for i in range(args.warmup):
         step()
@@ -179,7 +179,7 @@ def main():
                                    f"{args.spp}spp_d{args.depth}",
                        "scene": args.scene, "spheres": nspheres, "width": args.width,
                        "height": args.height, "spp": args.spp, "max_depth": args.depth,
-                       "parallelism": f"row-interleave{args.stripe}x{world}",
+                       "parallelism": f"tiles8x8-roundrobin-x{world}",
                        "accumulate_chunk": st["accumulate_chunk"],
                        "kernel_variant": st["kernel_variant"],
                        "grid_blocks": st["grid_blocks"]},

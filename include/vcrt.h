@@ -18,7 +18,7 @@
  *                            globals.glsl:9-24, include/Common.hpp:23-24
  *
  * Added (the reference has no equivalents): read-back of the rgba32f framebuffer, statistics,
- * rank/world stripe sharding and the stripe re-assembly used after a multi-GPU gather.
+ * rank/world tile sharding and the tile re-assembly used after a multi-GPU gather.
  *
  * Conventions: plain C types and pointers only. Every function returns a VkResult-compatible
  * int32_t (0 = success, negative = error; values from the Vulkan registry). Nothing throws
@@ -81,12 +81,13 @@ typedef struct vcrt_render_desc {
     int32_t max_depth;         /* MAX_RECURSION_LEVEL, >= 0 */
     vcrt_camera camera;
     int32_t device;        /* HIP device ordinal; -1 = current device */
-    int32_t rank;          /* this process's shard of the frame */
+    int32_t rank;          /* this process's shard of the frame: the 8x8 tiles t (row-major
+                              tile index) with t % world_size == rank */
     int32_t world_size;    /* number of shards (GPUs) */
-    int32_t stripe_height; /* rows per interleaved stripe; 0 = 1 (row interleave) */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
-    int32_t accumulate_chunk; /* samples per work item (0 = 16). A pixel's samples are summed
+    int32_t accumulate_chunk; /* samples per work item (0 = 16, halved down to 4 while the
+                                 rank has < 2^24 work items). A pixel's samples are summed
                                  in order within a chunk and the chunk sums in chunk order;
                                  >= samples_per_pixel reproduces the reference's sequential
                                  sum (shader.comp:46-54) exactly. */
@@ -102,7 +103,7 @@ typedef struct vcrt_stats {
     double resolve_ms;     /* chunk-sum resolve kernel time (0 when one chunk) */
     int32_t frames;        /* frames drawn since vcrt_begin */
     int32_t grid_blocks, block_threads, kernel_variant;
-    int32_t local_rows;    /* rows of this rank's packed framebuffer */
+    int32_t local_tiles;   /* 8x8 tiles this rank renders */
     int32_t nspheres;
     uint32_t lds_bytes;
     int32_t accumulate_chunk; /* samples per work item in effect */
@@ -119,21 +120,22 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count);
 vcrt_result vcrt_draw_next_frame(void);
 vcrt_result vcrt_end(void);
 
-/* Rows held by this rank: the rows y with (y / stripe_height) % world_size == rank, in order. */
-vcrt_result vcrt_local_rows(int32_t* rows);
-/* Copies the rank-local packed framebuffer (local_rows * width * 4 floats, rgba32f, row-major,
- * top row first) to host memory. count = number of floats available at rgba. */
+/* Rank-local framebuffer layout. world_size == 1: the frame, row-major [height][width] (row 0 =
+ * top, as the reference's storage image). world_size > 1: packed tiles [tiles][64] with element
+ * 8*(y%8) + x%8 of each tile (pixels outside the frame in edge tiles are left untouched). */
+vcrt_result vcrt_local_layout(uint32_t* elements, uint32_t* tiles);
+/* Copies the rank-local framebuffer (elements * 4 floats, rgba32f) to host memory; count = number
+ * of floats available at rgba. */
 vcrt_result vcrt_read_framebuffer(float* rgba, size_t count);
 /* Device address and size of the rank-local framebuffer (for collectives). */
 vcrt_result vcrt_framebuffer_device(void** device_ptr, size_t* bytes);
-/* Render into caller-owned device memory (>= local_rows*width*16 bytes); NULL = own buffer. */
+/* Render into caller-owned device memory (>= elements*16 bytes, 16-B aligned); NULL = own. */
 vcrt_result vcrt_set_framebuffer_device(void* device_ptr, size_t bytes);
-/* Rebuild a full frame from gathered rank framebuffers: gathered = [world][rows_per_rank][width]
- * float4, frame = [height][width] float4, both device pointers. Runs on the render stream and
- * returns when done. */
-vcrt_result vcrt_assemble_stripes(const void* gathered, void* frame, int32_t width,
-                                  int32_t height, int32_t world_size, int32_t stripe_height,
-                                  int32_t rows_per_rank);
+/* Rebuild the frame from gathered rank framebuffers: gathered = [world][tiles_per_rank][64]
+ * float4 (rank-major, each rank's packed tiles padded to tiles_per_rank), frame = [height][width]
+ * float4; both device pointers. Runs on the render stream and returns when done. */
+vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width, int32_t height,
+                                int32_t world_size, uint32_t tiles_per_rank);
 vcrt_result vcrt_get_stats(vcrt_stats* stats);
 
 /* Loads (or reloads) the tracer code object from a file; the analogue of

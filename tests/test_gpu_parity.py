@@ -20,10 +20,10 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0, world=1,
-               stripe=1, frames=1, scene_arr=None, chunk=0):
+               frames=1, scene_arr=None, chunk=0):
     desc = vc.RenderDesc(width=width, height=height, samples_per_pixel=spp, max_depth=depth,
-                         kernel_variant=variant, rank=rank, world_size=world,
-                         stripe_height=stripe, device=0, accumulate_chunk=chunk)
+                         kernel_variant=variant, rank=rank, world_size=world, device=0,
+                         accumulate_chunk=chunk)
     with vc.Renderer(desc, scene_arr if scene_arr is not None else scene) as r:
         for _ in range(frames):
             r.draw_next_frame()
@@ -57,8 +57,13 @@ CASES = [
 @pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
 @pytest.mark.parametrize("scene,w,h,spp,depth", CASES)
 def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
-    want, want_segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene(scene))
     got, st = gpu_render(scene, w, h, spp, depth, variant)
+    # default work split: the oracle sums in the same order (chunks of accumulate_chunk)
+    assert st["accumulate_chunk"] == vc.renderer.effective_chunk(spp, 0,
+                                                                 pixels=vc.tile_slots(w, h))
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth,
+                                                  chunk=st["accumulate_chunk"]),
+                                    oracle.scene(scene))
     assert got.shape == want.shape
     assert_bitwise(got, want, f"{scene} {w}x{h} spp{spp} d{depth} v{variant}")
     assert st["segments"] == want_segs
@@ -68,12 +73,12 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
 @pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
 @pytest.mark.parametrize("scene,w,h,spp,depth,chunk", [
     ("final", 64, 36, 64, 10, 16),   # 4 chunks
-    ("final", 48, 30, 40, 10, 0),    # default chunk 16: chunks of 16 + 16 + 8 (ragged)
+    ("final", 48, 30, 40, 10, 0),    # default chunk for a tiny frame: 4 (10 chunks)
     ("three", 72, 40, 96, 8, 7),     # 14 chunks, last one of 5
     ("final", 40, 24, 33, 10, 33),   # one chunk = the reference's sequential order
 ])
 def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, variant):
-    k = vc.renderer.effective_chunk(spp, chunk)
+    k = vc.renderer.effective_chunk(spp, chunk, pixels=vc.tile_slots(w, h))
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
     got, st = gpu_render(scene, w, h, spp, depth, variant, chunk=chunk)
     assert st["accumulate_chunk"] == k
@@ -142,27 +147,41 @@ def test_frames_are_identical(oracle):
     assert_bitwise(a, b, "frame 2 vs frame 1")
 
 
-@pytest.mark.parametrize("world,stripe", [(2, 1), (3, 1), (8, 1), (2, 16), (3, 16), (4, 5)])
-def test_sharded_stripes_reassemble_bitwise(world, stripe):
+@pytest.mark.parametrize("world", [2, 3, 8, 5])
+def test_sharded_tiles_reassemble_bitwise(world):
     import torch
-    w, h, spp, depth = 72, 90, 2, 10
+    w, h, spp, depth = 75, 46, 2, 10  # ragged: edge tiles are partial
     full, _ = gpu_render("final", w, h, spp, depth)
-    rows_per_rank = max(len(vc.rows_for_rank(h, stripe, world, r)) for r in range(world))
-    gathered = torch.zeros((world, rows_per_rank, w, 4), dtype=torch.float32, device="cuda:0")
-    segs = 0
+    pad = max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
+    m = vc.tile_pixel_map(w, h, world)
+    gathered = torch.zeros((world, pad * 64, 4), dtype=torch.float32, device="cuda:0")
     for rank in range(world):
-        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world, stripe=stripe)
-        rows = vc.rows_for_rank(h, stripe, world, rank)
-        assert part.shape == (len(rows), w, 4)
-        assert_bitwise(part, full[rows], f"rank {rank}/{world}")
-        gathered[rank, :len(rows)] = torch.from_numpy(part).to("cuda:0")
-        segs += st["segments"]
+        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world)
+        ntiles = len(vc.tiles_for_rank(w, h, world, rank))
+        assert part.shape == (ntiles, 64, 4) and st["local_tiles"] == ntiles
+        mine = m[..., 0] == rank
+        flat = part.reshape(-1, 4)
+        assert_bitwise(flat[m[..., 1][mine]], full[mine], f"rank {rank}/{world}")
+        gathered[rank, :ntiles * 64] = torch.from_numpy(flat).to("cuda:0")
     frame = torch.empty((h, w, 4), dtype=torch.float32, device="cuda:0")
-    desc = vc.RenderDesc(width=w, height=h, world_size=world, stripe_height=stripe, device=0)
+    desc = vc.RenderDesc(width=w, height=h, world_size=world, device=0)
     with vc.Renderer(desc) as r:
-        r.assemble_stripes(gathered.data_ptr(), frame.data_ptr(), rows_per_rank)
+        r.assemble_tiles(gathered.data_ptr(), frame.data_ptr(), pad)
+        with pytest.raises(vc.VcrtError):
+            r.assemble_tiles(gathered.data_ptr(), frame.data_ptr(), pad - 1)
     torch.cuda.synchronize()
     assert_bitwise(frame.cpu().numpy(), full, "assembled")
+
+
+def test_sharded_chunked_render_matches_oracle(oracle):
+    # a rank shard with several sample chunks (resolve kernel on packed tiles)
+    w, h, spp, depth, world = 64, 40, 24, 10, 3
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=8), oracle.scene("final"))
+    m = vc.tile_pixel_map(w, h, world)
+    for rank in range(world):
+        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world, chunk=8)
+        mine = m[..., 0] == rank
+        assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], f"rank {rank}")
 
 
 def test_render_into_external_device_buffer():
@@ -213,7 +232,8 @@ def test_full_size_rows_subset_rms(oracle):
     w, h, spp, depth = 1920, 1080, 16, 10
     got, st = gpu_render("final", w, h, spp, depth)
     rows = range(7, h, 90)
-    want, _ = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("final"), rows=rows)
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"]),
+                            oracle.scene("final"), rows=rows)
     sel = list(rows)
     g, o = got[sel].astype(np.float64), want[sel].astype(np.float64)
     rms = np.sqrt(((g - o) ** 2).mean(axis=(0, 1)))

@@ -41,7 +41,7 @@ def test_struct_layouts():
     assert d.struct_size == ctypes.sizeof(N.vcrt_render_desc)
     assert (d.width, d.height, d.samples_per_pixel, d.max_depth) == (1280, 720, 1, 50)
     assert list(d.camera.lookfrom) == [13, 2, 3] and d.camera.vfov == 20
-    assert (d.rank, d.world_size, d.stripe_height) == (0, 1, 1)
+    assert (d.rank, d.world_size) == (0, 1)
 
 
 def test_product_canonical_math_equals_oracle(oracle):
@@ -123,10 +123,19 @@ def test_python_lifecycle_mirror_returns_codes_without_gpu():
     assert vc.EndRenderingOperation() == 0
 
 
-@pytest.mark.parametrize("height,stripe,world", [(1080, 16, 8), (450, 16, 3), (7, 16, 2),
-                                                 (144, 8, 5), (2160, 16, 8)])
-def test_stripe_partition_is_exact(height, stripe, world):
+@pytest.mark.parametrize("w,h,world", [(1920, 1080, 8), (450, 200, 3), (7, 5, 2), (144, 81, 5),
+                                        (3840, 2160, 8), (33, 17, 4)])
+def test_tile_partition_is_exact(w, h, world):
+    ntiles = ((w + 7) // 8) * ((h + 7) // 8)
     seen = []
     for r in range(world):
-        seen += vc.rows_for_rank(height, stripe, world, r)
-    assert sorted(seen) == list(range(height))
+        seen += vc.tiles_for_rank(w, h, world, r)
+    assert sorted(seen) == list(range(ntiles))
+    counts = [len(vc.tiles_for_rank(w, h, world, r)) for r in range(world)]
+    assert max(counts) - min(counts) <= 1 and counts[0] == max(counts)
+    m = vc.tile_pixel_map(w, h, world)
+    # every (rank, element) is hit once and lies inside that rank's packed buffer
+    flat = m[..., 0].astype(np.int64) * (64 * max(counts)) + m[..., 1]
+    assert len(np.unique(flat)) == w * h
+    for r in range(world):
+        assert np.all(m[m[..., 0] == r][:, 1] < 64 * counts[r])

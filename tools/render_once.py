@@ -24,13 +24,12 @@ def main():
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--rank", type=int, default=0)
     p.add_argument("--world", type=int, default=1)
-    p.add_argument("--stripe", type=int, default=1)
     a = p.parse_args()
     desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
                          max_depth=a.depth, kernel_variant=a.variant,
                          blocks_per_cu=a.blocks_per_cu, device=0,
                          code_object_path=a.code_object, accumulate_chunk=a.chunk,
-                         rank=a.rank, world_size=a.world, stripe_height=a.stripe)
+                         rank=a.rank, world_size=a.world)
     with vc.Renderer(desc, a.scene) as r:
         out = []
         for _ in range(a.frames):

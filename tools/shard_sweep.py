@@ -1,0 +1,32 @@
+"""Per-rank kernel time of an N-way tile-sharded frame, all ranks rendered one after another on
+this GPU: max over ranks is what strong scaling sees; sum vs the unsharded frame shows the
+per-rank fixed costs (launch, drain)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import vulkancomputeraytracing_amd as vc  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--spp", type=int, default=1024)
+p.add_argument("--worlds", default="2,4,8")
+a = p.parse_args()
+base = dict(width=1920, height=1080, samples_per_pixel=a.spp, max_depth=10, device=0)
+with vc.Renderer(vc.RenderDesc(**base), "final") as r:
+    r.draw_next_frame()
+    full = r.stats()["kernel_ms"]
+res = {"full_ms": full, "spp": a.spp}
+for world in [int(x) for x in a.worlds.split(",")]:
+    per = []
+    for rank in range(world):
+        with vc.Renderer(vc.RenderDesc(rank=rank, world_size=world, **base), "final") as r:
+            r.draw_next_frame()
+            st = r.stats()
+            per.append(st["kernel_ms"])
+    res[f"world{world}"] = {"per_rank_ms": [round(x, 2) for x in per], "max_ms": max(per),
+                            "sum_ms": sum(per), "chunk": st["accumulate_chunk"],
+                            "ideal_efficiency": full / (world * max(per))}
+    print(world, json.dumps(res[f"world{world}"]), file=sys.stderr)
+print(json.dumps(res))

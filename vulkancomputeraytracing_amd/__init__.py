@@ -9,12 +9,14 @@ from . import _native
 from ._native import (VK_SUCCESS, VK_ERROR_INITIALIZATION_FAILED, VcrtError, KERNEL_AUTO,
                       KERNEL_LDS, KERNEL_SMEM, TEXTURE_GLASS, TEXTURE_LAMBERTIAN, TEXTURE_METAL)
 from .renderer import (BeginRenderingOperation, DrawNextFrame, EndRenderingOperation, Renderer,
-                       RenderDesc, SetRenderDescription, SetRenderScene, render, rows_for_rank)
+                       RenderDesc, SetRenderDescription, SetRenderScene, render, tile_pixel_map,
+                       tile_slots, tiles_for_rank)
 from .scene import SPHERE_DTYPE, builtin_scene, make_spheres, scene_generator_text
 
 __all__ = [
     "BeginRenderingOperation", "DrawNextFrame", "EndRenderingOperation", "Renderer",
-    "RenderDesc", "SetRenderDescription", "SetRenderScene", "render", "rows_for_rank",
+    "RenderDesc", "SetRenderDescription", "SetRenderScene", "render", "tiles_for_rank",
+    "tile_slots", "tile_pixel_map",
     "SPHERE_DTYPE", "builtin_scene", "make_spheres", "scene_generator_text", "VcrtError",
     "VK_SUCCESS", "VK_ERROR_INITIALIZATION_FAILED", "KERNEL_AUTO", "KERNEL_LDS", "KERNEL_SMEM",
     "TEXTURE_GLASS", "TEXTURE_LAMBERTIAN", "TEXTURE_METAL", "_native",

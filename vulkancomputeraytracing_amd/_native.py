@@ -68,7 +68,6 @@ class vcrt_render_desc(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("rank", ctypes.c_int32),
         ("world_size", ctypes.c_int32),
-        ("stripe_height", ctypes.c_int32),
         ("kernel_variant", ctypes.c_int32),
         ("blocks_per_cu", ctypes.c_int32),
         ("accumulate_chunk", ctypes.c_int32),
@@ -88,7 +87,7 @@ class vcrt_stats(ctypes.Structure):
         ("grid_blocks", ctypes.c_int32),
         ("block_threads", ctypes.c_int32),
         ("kernel_variant", ctypes.c_int32),
-        ("local_rows", ctypes.c_int32),
+        ("local_tiles", ctypes.c_int32),
         ("nspheres", ctypes.c_int32),
         ("lds_bytes", ctypes.c_uint32),
         ("accumulate_chunk", ctypes.c_int32),
@@ -103,13 +102,14 @@ SIGNATURES = {
     "vcrt_set_scene": (ctypes.c_int32, [ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_draw_next_frame": (ctypes.c_int32, []),
     "vcrt_end": (ctypes.c_int32, []),
-    "vcrt_local_rows": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32)]),
+    "vcrt_local_layout": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_uint32)]),
     "vcrt_read_framebuffer": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_size_t]),
     "vcrt_framebuffer_device": (
         ctypes.c_int32, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]),
     "vcrt_set_framebuffer_device": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_size_t]),
-    "vcrt_assemble_stripes": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p] +
-                              [ctypes.c_int32] * 5),
+    "vcrt_assemble_tiles": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p] +
+                            [ctypes.c_int32] * 3 + [ctypes.c_uint32]),
     "vcrt_get_stats": (ctypes.c_int32, [ctypes.POINTER(vcrt_stats)]),
     "vcrt_shader_load": (ctypes.c_int32, [ctypes.c_char_p]),
     "vcrt_scene_builtin": (ctypes.c_int32,

@@ -31,7 +31,7 @@ namespace {
 using vcrt::to_vk;
 
 constexpr size_t kCounterBytes = 256;  // work counter (u32) + segment counter (u64), padded
-constexpr int32_t kDefaultChunk = 16;        // samples per work item
+constexpr int32_t kDefaultChunk = 16;        // samples per work item (upper end)
 constexpr uint32_t kSmemTableBytes = 16384;  // scan table size served from the scalar cache
 
 struct RendererState {
@@ -66,7 +66,9 @@ struct RendererState {
     float4* d_fb = nullptr;  // current render target (own or caller-provided)
     size_t fb_bytes = 0;
     void* d_counters = nullptr;
-    int32_t local_rows = 0;
+    uint32_t tiles_x = 0, local_tiles = 0;
+    uint32_t local_elems = 0;   // float4 elements of the rank-local framebuffer
+    uint64_t local_pixels = 0;  // frame pixels this rank renders
     vcrt::Camera cam{};
     vcrt_stats stats{};
 };
@@ -79,17 +81,29 @@ RendererState g;
         if (e_ != hipSuccess) return to_vk(e_); \
     } while (0)
 
-int32_t rows_for_rank(int32_t height, int32_t stripe, int32_t world, int32_t rank) {
-    int32_t rows = 0;
-    for (int32_t s = rank; s * stripe < height; s += world)
-        rows += std::min(stripe, height - s * stripe);
-    return rows;
+// Samples per work item when the caller leaves it to us: 16, halved (down to 4) while the
+// rank's work would be fewer than 2^24 items, so every lane of the persistent grid (~400k
+// lanes on MI355X) still gets ~40 items and the drain at the end stays short. A function of
+// the configuration only, so the summation order does not depend on the device.
+int32_t default_chunk(uint64_t pixels, int32_t spp) {
+    int32_t k = kDefaultChunk;
+    while (k > 4 && pixels * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 24))
+        k /= 2;
+    return k;
+}
+
+// 8x8 tiles of a W x H frame owned by `rank` when tile t goes to rank t % world.
+uint32_t tiles_for_rank(int32_t width, int32_t height, int32_t world, int32_t rank) {
+    const uint64_t tiles = static_cast<uint64_t>((width + 7) / 8) * ((height + 7) / 8);
+    return tiles > static_cast<uint64_t>(rank)
+               ? static_cast<uint32_t>((tiles - rank + world - 1) / world)
+               : 0u;
 }
 
 // Directory of this shared object (for the default code-object path).
 std::string library_dir() {
     Dl_info info;
-    if (dladdr(reinterpret_cast<void*>(&rows_for_rank), &info) && info.dli_fname) {
+    if (dladdr(reinterpret_cast<void*>(&tiles_for_rank), &info) && info.dli_fname) {
         std::string p(info.dli_fname);
         const size_t slash = p.find_last_of('/');
         if (slash != std::string::npos) return p.substr(0, slash);
@@ -146,7 +160,7 @@ bool desc_valid(const vcrt_render_desc& d) {
         return false;
     if (static_cast<int64_t>(d.width) * d.height > (int64_t{1} << 31)) return false;
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
-    if (d.stripe_height < 0 || d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
+    if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
     if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_SMEM) return false;
     return true;
 }
@@ -178,7 +192,6 @@ vcrt_result vcrt_default_desc(vcrt_render_desc* d) {
     d->device = -1;
     d->rank = 0;
     d->world_size = 1;
-    d->stripe_height = 1;  // row interleave: best rank balance (multi-GPU)
     d->kernel_variant = VCRT_KERNEL_AUTO;
     return VCRT_SUCCESS;
 }
@@ -188,7 +201,6 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (g.begun) vcrt_end();
     g = RendererState{};
     g.desc = *desc;
-    if (g.desc.stripe_height == 0) g.desc.stripe_height = 1;
     g.begun = true;  // from here on vcrt_end() cleans up whatever was created
 
     int count = 0;
@@ -242,22 +254,35 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
                              hipMemcpyHostToDevice))) != VK_SUCCESS)
         return fail(r);
 
-    g.local_rows = rows_for_rank(g.desc.height, g.desc.stripe_height, g.desc.world_size,
-                                 g.desc.rank);
-    g.fb_bytes = static_cast<size_t>(g.local_rows) * g.desc.width * sizeof(float4);
+    // Frame sharding: 8x8 tiles, tile t to rank t % world (DESIGN.md "Multi-GPU").
+    g.tiles_x = static_cast<uint32_t>((g.desc.width + 7) / 8);
+    g.local_tiles = tiles_for_rank(g.desc.width, g.desc.height, g.desc.world_size, g.desc.rank);
+    g.local_elems = g.desc.world_size == 1
+                        ? static_cast<uint32_t>(g.desc.width) * static_cast<uint32_t>(g.desc.height)
+                        : g.local_tiles * 64u;
+    g.fb_bytes = static_cast<size_t>(g.local_elems) * sizeof(float4);
+    for (uint64_t t = static_cast<uint64_t>(g.desc.rank), ntiles = uint64_t{g.tiles_x} *
+                                                            ((g.desc.height + 7) / 8);
+         t < ntiles; t += static_cast<uint64_t>(g.desc.world_size)) {
+        const uint64_t tx = t % g.tiles_x, ty = t / g.tiles_x;
+        g.local_pixels += std::min<uint64_t>(8, g.desc.width - 8 * tx) *
+                          std::min<uint64_t>(8, g.desc.height - 8 * ty);
+    }
     if (g.fb_bytes) {
         if ((r = to_vk(hipMalloc(&g.d_fb_own, g.fb_bytes))) != VK_SUCCESS) return fail(r);
         if ((r = to_vk(hipMemset(g.d_fb_own, 0, g.fb_bytes))) != VK_SUCCESS) return fail(r);
     }
     g.d_fb = g.d_fb_own;
-    // Work decomposition: (8x8 tile, chunk of K samples) items; chunk sums in a slab.
-    g.total_pixels = static_cast<uint32_t>(g.local_rows) * static_cast<uint32_t>(g.desc.width);
-    g.chunk = g.desc.accumulate_chunk > 0 ? g.desc.accumulate_chunk : kDefaultChunk;
+    // Work decomposition: (local tile, chunk of K samples) items; chunk sums in a slab.
+    g.total_pixels = g.local_tiles * 64u;  // local element slots incl. partial-tile padding
+    g.chunk = g.desc.accumulate_chunk > 0
+                  ? g.desc.accumulate_chunk
+                  : default_chunk(static_cast<uint64_t>(g.total_pixels), spp);
     if (g.chunk > spp) g.chunk = spp;
     g.nchunks = (spp + g.chunk - 1) / g.chunk;
     {
-        const uint64_t tiles = (static_cast<uint64_t>(g.total_pixels) + 63) / 64;
-        const uint64_t items = tiles * 64 * static_cast<uint64_t>(g.nchunks);
+        const uint64_t items =
+            static_cast<uint64_t>(g.total_pixels) * static_cast<uint64_t>(g.nchunks);
         if (items >= (uint64_t{1} << 31)) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
         g.total_items = static_cast<uint32_t>(items);
     }
@@ -276,7 +301,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     vcrt::builtin_scene(VCRT_SCENE_FINAL, world);
     if ((r = vcrt_set_scene(world.data(), static_cast<int32_t>(world.size()))) != VK_SUCCESS)
         return fail(r);
-    g.stats.local_rows = g.local_rows;
+    g.stats.local_tiles = static_cast<int32_t>(g.local_tiles);
     g.stats.accumulate_chunk = g.chunk;
     return VCRT_SUCCESS;
 }
@@ -347,8 +372,8 @@ vcrt_result vcrt_draw_next_frame(void) {
     if (pixels != 0 && g.desc.max_depth == 0) {
         // ray_color with MAX_RECURSION_LEVEL 0 returns its undefined value (canonical 0) for
         // every sample without scanning: the frame is (0,0,0,1).
-        vcrt::FillParams fp{g.d_fb, pixels, make_float4(0.f, 0.f, 0.f, 1.f)};
-        const uint32_t grid = std::min<uint32_t>((pixels + 255) / 256, 4096);
+        vcrt::FillParams fp{g.d_fb, g.local_elems, make_float4(0.f, 0.f, 0.f, 1.f)};
+        const uint32_t grid = std::min<uint32_t>((g.local_elems + 255) / 256, 4096);
         VkResult r = launch(g.k_fill, grid, 256, 0, fp);
         if (r != VK_SUCCESS) return r;
     }
@@ -371,9 +396,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.max_depth = g.desc.max_depth;
         p.rank = g.desc.rank;
         p.world = g.desc.world_size;
-        p.stripe_h = g.desc.stripe_height;
-        p.local_rows = g.local_rows;
-        p.total_pixels = pixels;
+        p.tiles_x = g.tiles_x;
+        p.local_tiles = g.local_tiles;
         p.total_items = g.total_items;
         p.chunk = g.chunk;
         p.nchunks = g.nchunks;
@@ -418,8 +442,10 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
         if (g.nchunks > 1) {
-            vcrt::ResolveParams rp{g.d_partial, g.d_fb, pixels, g.nchunks,
-                                   g.desc.samples_per_pixel, g.desc.width, g.local_rows};
+            vcrt::ResolveParams rp{g.d_partial,  g.d_fb,        g.desc.width,
+                                   g.desc.height, g.desc.rank, g.desc.world_size,
+                                   g.tiles_x,     g.local_tiles, g.nchunks,
+                                   g.desc.samples_per_pixel};
             const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
             r = launch(g.k_resolve, rgrid, 256, 0, rp);
             if (r != VK_SUCCESS) return r;
@@ -448,7 +474,7 @@ vcrt_result vcrt_draw_next_frame(void) {
     VCRT_TRY(hipStreamSynchronize(g.stream));
     g.stats.sphere_tests = g.stats.segments * static_cast<uint64_t>(g.nspheres);
     g.stats.samples =
-        static_cast<uint64_t>(pixels) * static_cast<uint64_t>(g.desc.samples_per_pixel);
+        static_cast<uint64_t>(g.local_pixels) * static_cast<uint64_t>(g.desc.samples_per_pixel);
     g.stats.frames += 1;
     g.stats.frame_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -473,9 +499,10 @@ vcrt_result vcrt_end(void) {
     return VCRT_SUCCESS;
 }
 
-vcrt_result vcrt_local_rows(int32_t* rows) {
-    if (!g.begun || !rows) return VCRT_ERROR_INITIALIZATION_FAILED;
-    *rows = g.local_rows;
+vcrt_result vcrt_local_layout(uint32_t* elements, uint32_t* tiles) {
+    if (!g.begun || !elements || !tiles) return VCRT_ERROR_INITIALIZATION_FAILED;
+    *elements = g.local_elems;
+    *tiles = g.local_tiles;
     return VCRT_SUCCESS;
 }
 
@@ -505,17 +532,19 @@ vcrt_result vcrt_set_framebuffer_device(void* device_ptr, size_t bytes) {
     return VCRT_SUCCESS;
 }
 
-vcrt_result vcrt_assemble_stripes(const void* gathered, void* frame, int32_t width,
-                                  int32_t height, int32_t world_size, int32_t stripe_height,
-                                  int32_t rows_per_rank) {
+vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width,
+                                int32_t height, int32_t world_size, uint32_t tiles_per_rank) {
     if (!g.begun || !gathered || !frame) return VCRT_ERROR_INITIALIZATION_FAILED;
-    if (width <= 0 || height <= 0 || world_size <= 0 || stripe_height <= 0)
-        return VCRT_ERROR_INITIALIZATION_FAILED;
-    for (int32_t r = 0; r < world_size; r++)
-        if (rows_for_rank(height, stripe_height, world_size, r) > rows_per_rank)
-            return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
-    vcrt::AssembleParams ap{static_cast<const float4*>(gathered), static_cast<float4*>(frame),
-                            width, height, world_size, stripe_height, rows_per_rank};
+    if (width <= 0 || height <= 0 || world_size <= 0) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (tiles_for_rank(width, height, world_size, 0) > tiles_per_rank)
+        return VCRT_ERROR_FORMAT_NOT_SUPPORTED;  // rank 0 holds the most tiles
+    vcrt::AssembleParams ap{static_cast<const float4*>(gathered),
+                            static_cast<float4*>(frame),
+                            width,
+                            height,
+                            world_size,
+                            static_cast<uint32_t>((width + 7) / 8),
+                            tiles_per_rank};
     const uint64_t total = static_cast<uint64_t>(width) * height;
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((total + 255) / 256, 8192));
     VkResult r = launch(g.k_assemble, grid, 256, 0, ap);

@@ -122,25 +122,22 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
     }
 }
 
-// Work item -> pixel. Pixels are numbered q = 0..total-1 in 8-row bands, eight rows of one
-// column per 8 consecutive q, so 64 consecutive q form an 8x8 tile; local row lr maps to the
-// global row of this rank's interleaved stripes.
+// Local element q = 64 * lt + slot of this rank -> pixel (x, y) and its framebuffer index.
 struct Pixel {
-    uint32_t x, y, lr;
+    uint32_t x, y, out_index;
+    bool valid;  // edge tiles of frames that are not multiples of 8 are partial
 };
 
-__device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t local_rows,
-                                          uint32_t stripe_h, uint32_t world, uint32_t rank) {
-    const uint32_t band = q / (8u * W);
-    const uint32_t r = q - band * 8u * W;
-    const uint32_t rows_left = local_rows - band * 8u;
-    const uint32_t rows_in_band = rows_left < 8u ? rows_left : 8u;
+__device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, uint32_t tiles_x,
+                                          uint32_t world, uint32_t rank) {
+    const uint32_t lt = q >> 6, slot = q & 63u;
+    const uint32_t t = lt * world + rank;
+    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
     Pixel px;
-    px.x = r / rows_in_band;
-    px.lr = band * 8u + (r - px.x * rows_in_band);
-    const uint32_t ls = px.lr / stripe_h;
-    const uint32_t within = px.lr - ls * stripe_h;
-    px.y = (ls * world + rank) * stripe_h + within;
+    px.x = 8u * tx + (slot & 7u);
+    px.y = 8u * ty + (slot >> 3);
+    px.valid = px.x < W && px.y < H;
+    px.out_index = world == 1u ? px.y * W + px.x : q;
     return px;
 }
 
@@ -183,16 +180,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                     done = true;
                 } else {
                     if (reverse) item = p.total_items - 1u - item;
-                    // item = (tile, chunk, slot): 64 consecutive items = one tile x one chunk
+                    // item = (local tile, chunk, slot): 64 consecutive items = one tile x chunk
                     const uint32_t tile_chunk = item >> 6;
-                    const uint32_t tile = tile_chunk / nchunks;
-                    chunk = tile_chunk - tile * nchunks;
-                    q = tile * 64u + (item & 63u);
-                    if (q < p.total_pixels) {  // the last tile may be partial
-                        const Pixel px =
-                            pixel_of(q, (uint32_t)p.width, (uint32_t)p.local_rows,
-                                     (uint32_t)p.stripe_h, (uint32_t)p.world, (uint32_t)p.rank);
-                        out_index = px.lr * (uint32_t)p.width + px.x;
+                    const uint32_t lt = tile_chunk / nchunks;
+                    chunk = tile_chunk - lt * nchunks;
+                    q = lt * 64u + (item & 63u);
+                    const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
+                                              (uint32_t)p.world, (uint32_t)p.rank);
+                    if (px.valid) {
+                        out_index = px.out_index;
                         // shader.comp:43  pixel00 + x*delta_u + y*delta_v
                         pc = add(add(p00, scale((float)px.x, du)), scale((float)px.y, dv));
                         acc = mk(0.f, 0.f, 0.f);
@@ -297,7 +293,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                     p.out[out_index] =
                         make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
                 else
-                    p.partial[(size_t)chunk * p.total_pixels + q] =
+                    p.partial[(size_t)chunk * (p.local_tiles * 64u) + q] =
                         make_float4(acc.x, acc.y, acc.z, 0.0f);
                 need = true;
             } else {
@@ -355,32 +351,34 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem_stats(TracePar
 // Chunk sums -> pixels in chunk order: ((P0 + P1) + P2) + ..., then / spp (shader.comp:56).
 extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) {
     const float spp_f = (float)p.spp;
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.total_pixels;
+    const uint32_t elems = p.local_tiles * 64u;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < elems;
          q += gridDim.x * blockDim.x) {
+        const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
+                                  (uint32_t)p.world, (uint32_t)p.rank);
+        if (!px.valid) continue;
         float4 s = p.partial[q];
         for (int c = 1; c < p.nchunks; ++c) {
-            const float4 v = p.partial[(size_t)c * p.total_pixels + q];
+            const float4 v = p.partial[(size_t)c * elems + q];
             s.x = s.x + v.x;
             s.y = s.y + v.y;
             s.z = s.z + v.z;
         }
-        const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.local_rows, 1u, 1u, 0u);
-        p.out[px.lr * (uint32_t)p.width + px.x] =
-            make_float4(s.x / spp_f, s.y / spp_f, s.z / spp_f, 1.0f);
+        p.out[px.out_index] = make_float4(s.x / spp_f, s.y / spp_f, s.z / spp_f, 1.0f);
     }
 }
 
-// Reassemble the rank-interleaved stripes gathered from every rank into one frame.
+// Re-interleave the packed tile framebuffers gathered from every rank into one frame.
 extern "C" __global__ __launch_bounds__(256) void vcrt_assemble(AssembleParams p) {
-    const uint32_t total = (uint32_t)p.width * (uint32_t)p.height;
+    const uint32_t W = (uint32_t)p.width;
+    const uint32_t total = W * (uint32_t)p.height;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += gridDim.x * blockDim.x) {
-        const uint32_t y = i / (uint32_t)p.width, x = i - y * (uint32_t)p.width;
-        const uint32_t s = y / (uint32_t)p.stripe_h, within = y - s * (uint32_t)p.stripe_h;
-        const uint32_t r = s % (uint32_t)p.world;
-        const uint32_t lr = (s / (uint32_t)p.world) * (uint32_t)p.stripe_h + within;
-        p.frame[i] =
-            p.gathered[((size_t)r * (uint32_t)p.rows_per_rank + lr) * (uint32_t)p.width + x];
+        const uint32_t y = i / W, x = i - y * W;
+        const uint32_t t = (y >> 3) * p.tiles_x + (x >> 3);
+        const uint32_t r = t % (uint32_t)p.world, lt = t / (uint32_t)p.world;
+        const uint32_t slot = ((y & 7u) << 3) | (x & 7u);
+        p.frame[i] = p.gathered[((size_t)r * p.tiles_per_rank + lt) * 64u + slot];
     }
 }
 

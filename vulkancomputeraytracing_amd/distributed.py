@@ -1,47 +1,37 @@
-"""Multi-GPU frame sharding: interleaved row stripes per rank + one framebuffer gather.
+"""Multi-GPU frame sharding: round-robin 8x8 tiles per rank + one framebuffer gather.
 
-One process per GPU. Rank r renders the rows y with (y // stripe) % world == r (SURVEY.md 8(e):
-interleaving balances cheap sky rows against expensive ground rows); the packed rank-local
-framebuffers (padded to the largest rank's row count) are all-gathered over RCCL
+One process per GPU. The frame is cut into 8x8 tiles (row-major tile index t); rank r renders
+the tiles with t % world == r, so every work item stays a coherent 8x8 tile and every rank gets
+the same number of tiles spread over the whole frame (sky and ground alike: SURVEY.md 8(e)).
+The packed rank framebuffers [tiles_per_rank][64] are all-gathered over RCCL
 (``torch.distributed`` backend "nccl") and rank 0 re-interleaves them with the vcrt_assemble
 HIP kernel. The reference is single-GPU (Environment.cpp:157-165; "TODO: Cross-GPU sharing",
 Frontend.cpp:107); the gather is the one exchange step of the path.
 """
 from __future__ import annotations
 
-import numpy as np
-
-from .renderer import rows_for_rank
+from .renderer import tile_pixel_map, tiles_for_rank  # noqa: F401  (re-exported)
 
 
-def rows_per_rank(height: int, stripe: int, world: int) -> int:
-    """Rows of the largest rank: the padded per-rank slab of the gather."""
-    return max(len(rows_for_rank(height, stripe, world, r)) for r in range(world))
+def tiles_per_rank(width: int, height: int, world: int) -> int:
+    """Tiles of the largest rank (rank 0): the padded per-rank slab of the gather."""
+    return len(tiles_for_rank(width, height, world, 0))
 
 
-def stripe_row_map(height: int, stripe: int, world: int) -> np.ndarray:
-    """For each global row y: (owning rank, row index in that rank's packed framebuffer).
-    The host-side statement of the index map vcrt_assemble applies on the GPU."""
-    y = np.arange(height)
-    s = y // stripe
-    rank = s % world
-    local = (s // world) * stripe + y % stripe
-    return np.stack([rank, local], axis=1)
-
-
-def gather_stripes(local, rows_pad: int, group=None):
-    """All-gather the ranks' packed framebuffers. `local` is [rows_pad, W, 4] (rows past the
-    rank's own count are padding). Returns [world * rows_pad, W, 4] (rank-major)."""
+def gather_tiles(local, tiles_pad: int, group=None):
+    """All-gather the ranks' packed tile framebuffers. `local` is [tiles_pad * 64, 4] float
+    (tiles past the rank's own count are padding). Returns [world * tiles_pad * 64, 4],
+    rank-major."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    assert local.shape[0] == rows_pad and local.is_contiguous()
-    out = torch.empty((world * rows_pad,) + tuple(local.shape[1:]), dtype=local.dtype,
+    assert local.shape[0] == tiles_pad * 64 and local.is_contiguous()
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
     dist.all_gather_into_tensor(out, local, group=group)
     return out
 
 
-def assemble_frame(renderer, gathered, frame, rows_pad: int) -> None:
-    """Re-interleave gathered stripes into `frame` [H, W, 4] on the GPU (vcrt_assemble)."""
-    renderer.assemble_stripes(gathered.data_ptr(), frame.data_ptr(), rows_pad)
+def assemble_frame(renderer, gathered, frame, tiles_pad: int) -> None:
+    """Re-interleave gathered tiles into `frame` [H, W, 4] on the GPU (vcrt_assemble)."""
+    renderer.assemble_tiles(gathered.data_ptr(), frame.data_ptr(), tiles_pad)

@@ -29,8 +29,7 @@ class RenderDesc:
     vfov: float = 20.0
     device: int = -1
     rank: int = 0
-    world_size: int = 1
-    stripe_height: int = 1          # rows per interleaved stripe (1 = row interleave)
+    world_size: int = 1             # shards: rank owns the 8x8 tiles t with t % world == rank
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
     accumulate_chunk: int = 0       # 0 = 16; >= spp: the reference's sequential order
@@ -48,7 +47,6 @@ class RenderDesc:
         d.camera.vfov = float(self.vfov)
         d.device = self.device
         d.rank, d.world_size = self.rank, self.world_size
-        d.stripe_height = self.stripe_height
         d.kernel_variant = self.kernel_variant
         d.blocks_per_cu = self.blocks_per_cu
         d.accumulate_chunk = self.accumulate_chunk
@@ -61,15 +59,37 @@ class RenderDesc:
 DEFAULT_ACCUMULATE_CHUNK = 16
 
 
-def effective_chunk(spp: int, accumulate_chunk: int = 0) -> int:
-    """Samples per work item the renderer uses (the oracle's `chunk` for the same order)."""
-    k = accumulate_chunk if accumulate_chunk > 0 else DEFAULT_ACCUMULATE_CHUNK
+def effective_chunk(spp: int, accumulate_chunk: int = 0, pixels: int | None = None) -> int:
+    """Samples per work item the renderer uses (the oracle's `chunk` for the same order).
+    Mirrors default_chunk() in csrc/capi.cpp when accumulate_chunk is 0; `pixels` is the
+    rank's tile slots (64 per 8x8 tile, see tile_slots)."""
+    if accumulate_chunk > 0:
+        k = accumulate_chunk
+    else:
+        k = DEFAULT_ACCUMULATE_CHUNK
+        if pixels is not None:
+            while k > 4 and pixels * (-(-spp // k)) < (1 << 24):
+                k //= 2
     return min(k, spp)
 
 
-def rows_for_rank(height: int, stripe: int, world: int, rank: int) -> list[int]:
-    """Global rows owned by `rank`: stripe s = y // stripe belongs to rank s % world."""
-    return [y for y in range(height) if (y // stripe) % world == rank]
+def tiles_for_rank(width: int, height: int, world: int, rank: int) -> list[int]:
+    """Row-major 8x8 tile indices rank `rank` renders: t % world == rank."""
+    ntiles = ((width + 7) // 8) * ((height + 7) // 8)
+    return list(range(rank, ntiles, world))
+
+
+def tile_slots(width: int, height: int, world: int = 1, rank: int = 0) -> int:
+    """64 work slots per owned tile (edge tiles included whole)."""
+    return 64 * len(tiles_for_rank(width, height, world, rank))
+
+
+def tile_pixel_map(width: int, height: int, world: int) -> np.ndarray:
+    """For every frame pixel [y, x]: (rank, element index in that rank's packed tile buffer).
+    The host statement of the index map the vcrt_assemble kernel applies."""
+    y, x = np.mgrid[0:height, 0:width]
+    t = (y // 8) * ((width + 7) // 8) + x // 8
+    return np.stack([t % world, (t // world) * 64 + (y % 8) * 8 + x % 8], axis=-1)
 
 
 # ---- reference-named lifecycle (VkResult codes, no exceptions) ----------------------------
@@ -144,15 +164,19 @@ class Renderer:
     def draw_next_frame(self) -> None:
         N.check("vcrt_draw_next_frame", self._lib.vcrt_draw_next_frame())
 
-    @property
-    def local_rows(self) -> int:
-        v = ctypes.c_int32()
-        N.check("vcrt_local_rows", self._lib.vcrt_local_rows(ctypes.byref(v)))
-        return v.value
+    def local_layout(self) -> tuple[int, int]:
+        """(float4 elements, tiles) of the rank-local framebuffer."""
+        e, t = ctypes.c_uint32(), ctypes.c_uint32()
+        N.check("vcrt_local_layout", self._lib.vcrt_local_layout(ctypes.byref(e), ctypes.byref(t)))
+        return e.value, t.value
 
     def read_framebuffer(self) -> np.ndarray:
-        """Rank-local framebuffer as float32 [local_rows, width, 4] (rgba32f, top row first)."""
-        out = np.empty((self.local_rows, self.desc.width, 4), dtype=np.float32)
+        """Rank-local framebuffer, float32 rgba: world 1 -> [height, width, 4] (top row first);
+        world > 1 -> packed tiles [tiles, 64, 4] (element 8*(y%8) + x%8)."""
+        elems, tiles = self.local_layout()
+        shape = ((self.desc.height, self.desc.width, 4) if self.desc.world_size == 1
+                 else (tiles, 64, 4))
+        out = np.empty(shape, dtype=np.float32)
         N.check("vcrt_read_framebuffer", self._lib.vcrt_read_framebuffer(
             out.ctypes.data_as(ctypes.c_void_p), out.size))
         return out
@@ -167,11 +191,11 @@ class Renderer:
         N.check("vcrt_set_framebuffer_device",
                 self._lib.vcrt_set_framebuffer_device(ctypes.c_void_p(ptr or None), nbytes))
 
-    def assemble_stripes(self, gathered_ptr: int, frame_ptr: int, rows_per_rank: int) -> None:
+    def assemble_tiles(self, gathered_ptr: int, frame_ptr: int, tiles_per_rank: int) -> None:
         d = self.desc
-        N.check("vcrt_assemble_stripes", self._lib.vcrt_assemble_stripes(
+        N.check("vcrt_assemble_tiles", self._lib.vcrt_assemble_tiles(
             ctypes.c_void_p(gathered_ptr), ctypes.c_void_p(frame_ptr), d.width, d.height,
-            d.world_size, d.stripe_height, rows_per_rank))
+            d.world_size, tiles_per_rank))
 
     def shader_load(self, path: str) -> None:
         N.check("vcrt_shader_load", self._lib.vcrt_shader_load(path.encode()))
