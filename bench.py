@@ -61,10 +61,16 @@ def cpu_baseline(args):
     dt = max(time.perf_counter() - t0, 1e-3)
     rate = len(probe_rows) * args.width * probe_spp / dt  # samples/s
     target = rate * args.cpu_seconds
-    spp = max(1, min(args.spp, 16))
-    nrows = max(1, min(args.height, int(target / (args.width * spp))))
-    step = max(1, args.height // nrows)
-    rows = range(0, args.height, step)
+    frame = args.width * args.height
+    if target >= 4 * frame:  # whole frame at the first spp samples
+        spp = max(4, min(args.spp, int(target // frame)))
+        rows = range(0, args.height)
+        step = 1
+    else:                    # every step-th row at 4 spp
+        spp = min(args.spp, 4)
+        nrows = max(1, int(target / (args.width * spp)))
+        step = max(1, args.height // nrows)
+        rows = range(0, args.height, step)
     t0 = time.perf_counter()
     o.render(o.config(args.width, args.height, spp, args.depth), scene, rows=rows, threads=threads)
     dt = time.perf_counter() - t0
