@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--validate", action="store_true",
+                   help="rank 0 re-renders the frame on one GPU after the timed steps and checks "
+                        "the gathered frame bit for bit (use with an explicit --chunk)")
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU work for the cpu_baseline sample")
     return p.parse_args()
@@ -96,15 +99,22 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; VCRT_DIST_BACKEND=gloo rehearses the N > 1 flow with several ranks
+    # sharing the GPUs of a smaller box (RCCL needs one GPU per rank)
+    backend = os.environ.get("VCRT_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
-                         max_depth=args.depth, device=local_rank, rank=rank, world_size=world,
+                         max_depth=args.depth, device=device, rank=rank, world_size=world,
                          kernel_variant=args.variant,
                          blocks_per_cu=args.blocks_per_cu, accumulate_chunk=args.chunk)
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", device)
     tiles_pad = D.tiles_per_rank(args.width, args.height, world)
     local_elems = args.width * args.height if world == 1 else tiles_pad * 64
     local = torch.zeros((local_elems, 4), dtype=torch.float32, device=dev)
@@ -146,11 +156,24 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = r.stats()
     r.close()
+    validated = None
+    if args.validate and rank == 0:
+        import numpy as np
+        got = (frame if world > 1 else local.view(args.height, args.width, 4)).cpu().numpy()
+        ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
+                                 max_depth=args.depth, device=device, kernel_variant=args.variant,
+                                 accumulate_chunk=args.chunk)
+        with vc.Renderer(ref_desc, args.scene) as ref:
+            ref.draw_next_frame()
+            want = ref.read_framebuffer()
+        validated = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        log(f"validate: gathered frame bit-identical to a 1-GPU render: {validated}")
 
     if rank == 0:
         samples = args.width * args.height * args.spp * args.steps
@@ -197,6 +220,8 @@ def main():
                          "kernel_ms": round(k_ms, 3), "segments_per_launch": int(seg),
                          "flops_per_launch": flops},
         }
+        if validated is not None:
+            out["validated_bitwise_vs_1gpu"] = validated
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args)

@@ -79,6 +79,28 @@ __device__ __forceinline__ void accept_root(float hb, float disc, float a, float
     }
 }
 
+// Conservative pre-filter for the root path: false only when hit_sphere would certainly reject
+// the sphere, decided without the correctly rounded sqrt/divisions.
+//   sq_hi >= RN(sqrt(disc)): hardware v_sqrt_f32 (~1 ulp) plus 4 ulp;
+//   x1_lo = RN(-hb - sq_hi) <= x1 and x2_hi = RN(-hb + sq_hi) >= x2 (rounding is monotone);
+//   "beyond": x1_lo - max_t*a >= 0 (the sign of the fused fma is exact: every operand is a
+//   multiple of >= 2^-76 in the guarded ranges, so nothing underflows) => x1/a >= max_t =>
+//   root1 = RN(x1/a) >= max_t and root2 >= root1: both rejected;
+//   "behind": x2_hi - min_t*a <= 0 => root2 <= min_t and root1 <= root2: both rejected.
+// Outside the guarded ranges (tiny/huge/NaN values) it answers true and the exact path decides.
+__device__ __forceinline__ bool may_accept(float hb, float disc, float a, float max_t,
+                                           bool ray_ok) {
+    const float min_t = 0.001f;
+    const bool ok = ray_ok && disc >= 0x1p-100f && disc <= 0x1p100f && hb >= -0x1p60f &&
+                    hb <= 0x1p60f;
+    const float sq_hi = __uint_as_float(__float_as_uint(__builtin_amdgcn_sqrtf(disc)) + 4u);
+    const float x1_lo = -hb - sq_hi;
+    const float x2_hi = -hb + sq_hi;
+    const bool beyond = __builtin_fmaf(-max_t, a, x1_lo) >= 0.0f;
+    const bool behind = __builtin_fmaf(-min_t, a, x2_hi) <= 0.0f;
+    return !ok || !(beyond || behind);
+}
+
 // Discriminants of two spheres at once (hit_sphere's first half, element-wise exact):
 // oc = o - c; half_b = dot(oc, d); c = dot(oc, oc) - r²; disc = half_b² - a·c.
 __device__ __forceinline__ void pair_disc(const v2f ox, const v2f oy, const v2f oz, const v2f dx,
@@ -99,6 +121,14 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
                                              const f3 o, const f3 d, float& max_t, int& best,
                                              uint32_t& hit_groups) {
     const float a = dot(d, d);  // loop-invariant in hit_sphere: hoisting is exact
+    // the pre-filter's guarded range: a in [2^-20, 2^60] (and not NaN)
+    const bool ray_ok = a >= 0x1p-20f && a <= 0x1p60f;
+    // |o| <= 2^30 and a <= 2^60 (|d| <= 2^30) with the host-checked scene bound |c|, r <= 2^30
+    // keep every discriminant finite (hb^2, a*c < 2^127): no NaN can reach the max test
+    const bool finite_ok = (p.flags & kFlagSceneBounded) != 0 && a <= 0x1p60f &&
+                           fabsf(o.x) <= 0x1p30f && fabsf(o.y) <= 0x1p30f &&
+                           fabsf(o.z) <= 0x1p30f;
+    const uint64_t unguarded = __ballot(!finite_ok);
     const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     const int ngroups = (n + 3) >> 2;
@@ -108,15 +138,29 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
         v2f hb01, d01, hb23, d23;
         pair_disc(ox, oy, oz, dx, dy, dz, a2, g.q[0], g.q[1], hb01, d01);
         pair_disc(ox, oy, oz, dx, dy, dz, a2, g.q[2], g.q[3], hb23, d23);
-        const bool h0 = !(d01.x < 0.0f), h1 = !(d01.y < 0.0f), h2 = !(d23.x < 0.0f),
-                   h3 = !(d23.y < 0.0f);
-        if (__ballot(h0) | __ballot(h1) | __ballot(h2) | __ballot(h3)) {
+        // Any of the four not negative? For finite discriminants this is !(max < 0): one
+        // v_max3 + v_max + compare instead of four compares. Lanes whose ray is outside the
+        // guarded range (where a discriminant could be NaN, which max would drop) always take
+        // the exact per-sphere test below.
+        const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
+        if (__ballot(!(m4 < 0.0f)) | unguarded) {
+            const bool h0 = !(d01.x < 0.0f), h1 = !(d01.y < 0.0f), h2 = !(d23.x < 0.0f),
+                       h3 = !(d23.y < 0.0f);
             ++hit_groups;
             const int j = 4 * gi;  // padding spheres (index >= n) are never accepted
-            if (h0) accept_root(hb01.x, d01.x, a, max_t, best, j + 0);
-            if (h1 && j + 1 < n) accept_root(hb01.y, d01.y, a, max_t, best, j + 1);
-            if (h2 && j + 2 < n) accept_root(hb23.x, d23.x, a, max_t, best, j + 2);
-            if (h3 && j + 3 < n) accept_root(hb23.y, d23.y, a, max_t, best, j + 3);
+            // pre-filter against the max_t at group entry: a rejection stays valid as max_t
+            // only shrinks; survivors go through hit_sphere's exact logic in index order
+            const float mt = max_t;
+            const bool e0 = h0 && may_accept(hb01.x, d01.x, a, mt, ray_ok);
+            const bool e1 = h1 && j + 1 < n && may_accept(hb01.y, d01.y, a, mt, ray_ok);
+            const bool e2 = h2 && j + 2 < n && may_accept(hb23.x, d23.x, a, mt, ray_ok);
+            const bool e3 = h3 && j + 3 < n && may_accept(hb23.y, d23.y, a, mt, ray_ok);
+            if (__ballot(e0) | __ballot(e1) | __ballot(e2) | __ballot(e3)) {
+                if (e0) accept_root(hb01.x, d01.x, a, max_t, best, j + 0);
+                if (e1) accept_root(hb01.y, d01.y, a, max_t, best, j + 1);
+                if (e2) accept_root(hb23.x, d23.x, a, max_t, best, j + 2);
+                if (e3) accept_root(hb23.y, d23.y, a, max_t, best, j + 3);
+            }
         }
         g = nx;
     }

@@ -42,6 +42,7 @@ struct TraceParams {
 };
 
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
+constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 
 struct ResolveParams {
     const float4* partial;  // [nchunks][local_tiles * 64]

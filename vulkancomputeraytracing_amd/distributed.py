@@ -26,6 +26,9 @@ def gather_tiles(local, tiles_pad: int, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     assert local.shape[0] == tiles_pad * 64 and local.is_contiguous()
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal path (several ranks on one GPU): gloo gathers host copies
+        return gather_tiles(local.cpu(), tiles_pad, group).to(local.device)
     out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
     dist.all_gather_into_tensor(out, local, group=group)
