@@ -91,6 +91,11 @@ typedef struct vcrt_render_desc {
                                  in order within a chunk and the chunk sums in chunk order;
                                  >= samples_per_pixel reproduces the reference's sequential
                                  sum (shader.comp:46-54) exactly. */
+    int32_t progressive; /* 0: every DrawNextFrame re-renders samples 0..spp-1 (the reference,
+                            Linux.cpp:362-366). 1: frame f renders samples f*spp..(f+1)*spp-1 and
+                            the framebuffer holds the average of all frames so far (the same
+                            image as one render with (f+1)*spp samples and chunk boundaries at
+                            every frame; RENDER_ITERATION, Common.hpp:25, was never wired up). */
     const char* code_object_path; /* NULL = vcrt_tracer.hsaco next to libvcrt.so, then embedded */
 } vcrt_render_desc;
 
@@ -107,6 +112,7 @@ typedef struct vcrt_stats {
     int32_t nspheres;
     uint32_t lds_bytes;
     int32_t accumulate_chunk; /* samples per work item in effect */
+    uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
     uint64_t debug[8]; /* diagnostics (VCRT_DEBUG_STATS=1): wave-iterations, active-lane sum,
                           hit groups, fetches, last/first wave end time, sum end time, waves */
 } vcrt_stats;
@@ -137,6 +143,14 @@ vcrt_result vcrt_set_framebuffer_device(void* device_ptr, size_t bytes);
 vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width, int32_t height,
                                 int32_t world_size, uint32_t tiles_per_rank);
 vcrt_result vcrt_get_stats(vcrt_stats* stats);
+/* Progressive mode: drop the accumulated frames (sample sequence restarts at 0). */
+vcrt_result vcrt_reset_accumulation(void);
+/* The rank-local framebuffer encoded as sRGB8 RGBA (alpha linear), as the reference's
+ * B8G8R8A8_SRGB swapchain stores it at present time (Frontend.cpp:43; shader.frag:14 copies the
+ * texel): channel byte = round-to-nearest of 255 * sRGB(clamp(c, 0, 1)). bytes >= elements*4. */
+vcrt_result vcrt_read_framebuffer_srgb8(uint8_t* rgba8, size_t bytes);
+/* The 255 ascending linear thresholds behind that encode (byte = #{k : c >= t[k]}). */
+void vcrt_srgb8_thresholds(float thresholds[255]);
 
 /* Loads (or reloads) the tracer code object from a file; the analogue of
  * CreateShaderStageFromFile. Returns VCRT_ERROR_INCOMPATIBLE_SHADER_BINARY when the file

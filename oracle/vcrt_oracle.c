@@ -325,13 +325,17 @@ static void render_row(render_job* job, int y, uint64_t* segs) {
     v3 center = V(job->cam[9], job->cam[10], job->cam[11]);
     for (int x = 0; x < cfg->width; x++) {
         v3 pc = vadd(vadd(p00, vscale((float)x, du)), vscale((float)y, dv));
+        const int block = (cfg->frame_spp <= 0 || cfg->frame_spp > cfg->spp) ? cfg->spp
+                                                                            : cfg->frame_spp;
         const int chunk =
-            (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= cfg->spp) ? cfg->spp
-                                                                               : cfg->accumulate_chunk;
+            (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block) ? block
+                                                                            : cfg->accumulate_chunk;
         v3 acc = V(0.0f, 0.0f, 0.0f);
-        for (int c0 = 0; c0 < cfg->spp; c0 += chunk) {
+        for (int c0 = 0; c0 < cfg->spp;) {
             v3 part = V(0.0f, 0.0f, 0.0f);
-            const int c1 = c0 + chunk < cfg->spp ? c0 + chunk : cfg->spp;
+            const int block_end = (c0 / block + 1) * block;
+            int c1 = c0 + chunk < block_end ? c0 + chunk : block_end;
+            if (c1 > cfg->spp) c1 = cfg->spp;
             for (int i = c0; i < c1; i++) {
                 float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
                 v3 rs = vadd(vscale(jx, du), vscale(jy, dv));
@@ -340,6 +344,7 @@ static void render_row(render_job* job, int y, uint64_t* segs) {
                 part = vadd(part, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
             }
             acc = vadd(acc, part); /* one chunk: 0 + part == part, the sequential sum */
+            c0 = c1;
         }
         float* px = job->rgba + ((size_t)y * cfg->width + x) * 4;
         px[0] = acc.x / (float)cfg->spp;
@@ -407,6 +412,33 @@ int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t 
     free(jit);
     if (segments) *segments = job.segments;
     return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* presentation encode: linear -> sRGB8 (VK_FORMAT_B8G8R8A8_SRGB store, Frontend.cpp:43)     */
+
+static unsigned char srgb_byte(float c) {
+    if (!(c > 0.0f)) return 0; /* negative, zero, NaN */
+    if (c >= 1.0f) return 255;
+    /* round-to-nearest of 255 * encode(c): the largest k with encode(c) >= (k - 0.5)/255,
+     * evaluated as c >= inverse_encode((k - 0.5)/255) in double */
+    int lo = 0, hi = 255;
+    while (lo < hi) { /* count of thresholds <= c */
+        int mid = (lo + hi + 1) / 2;
+        double s = (mid - 0.5) / 255.0;
+        double lin = s <= 0.04045 ? s / 12.92 : pow((s + 0.055) / 1.055, 2.4);
+        if ((double)c >= lin) lo = mid; else hi = mid - 1;
+    }
+    return (unsigned char)lo;
+}
+
+void oracle_encode_srgb8(const float* rgba, size_t pixels, uint8_t* out) {
+    for (size_t i = 0; i < pixels; i++) {
+        for (int k = 0; k < 3; k++) out[4 * i + k] = srgb_byte(rgba[4 * i + k]);
+        float a = rgba[4 * i + 3];
+        a = a != a ? 0.0f : (a < 0.0f ? 0.0f : (a > 1.0f ? 1.0f : a));
+        out[4 * i + 3] = (uint8_t)(a * 255.0f + 0.5f);
+    }
 }
 
 /* ------------------------------------------------------------------------------------ */

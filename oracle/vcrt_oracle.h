@@ -38,6 +38,9 @@ typedef struct oracle_config {
      * K < spp: samples summed sequentially within chunks of K, chunk sums then added in chunk
      * order (the order the GPU uses when it splits a pixel's samples into work items). */
     int32_t accumulate_chunk;
+    /* Chunk boundaries also restart every frame_spp samples (progressive frames of frame_spp
+     * samples each); 0 = one frame of spp samples. */
+    int32_t frame_spp;
 } oracle_config;
 
 /* Canonical math (see DESIGN.md "canonical math"). */
@@ -58,6 +61,10 @@ int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t 
 /* Per-pixel radiance of one sample (ray_color), for KATs. */
 void oracle_ray_color(const oracle_sphere* world, int32_t n, const float origin[3],
                       const float dir[3], int32_t max_depth, float out[3], uint64_t* segments);
+
+/* Linear rgba32f -> sRGB8 RGBA as a B8G8R8A8_SRGB swapchain stores it (Frontend.cpp:43):
+ * channel byte = round-to-nearest of 255 * sRGB(clamp(c,0,1)), NaN -> 0, alpha linear. */
+void oracle_encode_srgb8(const float* rgba, size_t pixels, uint8_t* out);
 
 /* SceneGenerator.cpp:23-56 stdout, byte for byte. Returns bytes needed (excl. NUL). */
 size_t oracle_scene_generator_text(char* buf, size_t cap);

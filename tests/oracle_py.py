@@ -30,6 +30,7 @@ class OracleConfig(ctypes.Structure):
         ("lookfrom", ctypes.c_float * 3), ("lookat", ctypes.c_float * 3),
         ("vup", ctypes.c_float * 3), ("vfov", ctypes.c_float),
         ("accumulate_chunk", ctypes.c_int32),
+        ("frame_spp", ctypes.c_int32),
     ]
 
 
@@ -58,6 +59,8 @@ class Oracle:
         L.oracle_ray_color.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_encode_srgb8.restype = None
+        L.oracle_encode_srgb8.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.oracle_scene_generator_text.restype = ctypes.c_size_t
         L.oracle_scene_generator_text.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_scene_random_spheres.restype = ctypes.c_int32
@@ -73,9 +76,10 @@ class Oracle:
 
     @staticmethod
     def config(width, height, spp, max_depth, lookfrom=(13, 2, 3), lookat=(0, 0, 0),
-               vup=(0, 1, 0), vfov=20.0, chunk=0) -> OracleConfig:
+               vup=(0, 1, 0), vfov=20.0, chunk=0, frame_spp=0) -> OracleConfig:
         c = OracleConfig()
         c.accumulate_chunk = chunk
+        c.frame_spp = frame_spp
         c.width, c.height, c.spp, c.max_depth = width, height, spp, max_depth
         c.lookfrom[:] = [float(v) for v in lookfrom]
         c.lookat[:] = [float(v) for v in lookat]
@@ -105,6 +109,12 @@ class Oracle:
         if r != 0:
             raise ValueError("oracle_render rejected its arguments")
         return img, segs.value
+
+    def encode_srgb8(self, rgba: np.ndarray) -> np.ndarray:
+        rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+        out = np.zeros(rgba.shape, dtype=np.uint8)
+        self.lib.oracle_encode_srgb8(rgba.ctypes.data, rgba.size // 4, out.ctypes.data)
+        return out
 
     def ray_color(self, spheres, origin, direction, max_depth):
         spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)

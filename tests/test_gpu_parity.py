@@ -244,3 +244,39 @@ def test_full_size_rows_subset_rms(oracle):
     assert np.all(np.isfinite(got)) and np.all(got[..., :3] >= 0)
     assert st["samples"] == w * h * spp
     assert st["segments"] >= w * h * spp  # at least one segment per sample
+
+
+def test_srgb8_encode_bitwise(oracle):
+    w, h = 96, 54
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=4, max_depth=10, device=0)
+    with vc.Renderer(desc, "final") as r:
+        r.draw_next_frame()
+        lin = r.read_framebuffer()
+        srgb = r.read_framebuffer_srgb8()
+    assert srgb.shape == (h, w, 4) and srgb.dtype == np.uint8
+    assert np.array_equal(srgb, oracle.encode_srgb8(lin))
+    want, _ = oracle.render(oracle.config(w, h, 4, 10), oracle.scene("final"))
+    assert np.array_equal(srgb, oracle.encode_srgb8(want))
+
+
+@pytest.mark.parametrize("spp,chunk", [(4, 0), (6, 4), (3, 1)])
+def test_progressive_frames_bitwise(oracle, spp, chunk):
+    w, h, depth, frames = 48, 30, 10, 3
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         progressive=True, accumulate_chunk=chunk)
+    scene = oracle.scene("final")
+    with vc.Renderer(desc, "final") as r:
+        k = r.stats()["accumulate_chunk"]
+        outs = []
+        for f in range(frames):
+            r.draw_next_frame()
+            outs.append(r.read_framebuffer())
+            assert r.stats()["accumulated_spp"] == (f + 1) * spp
+        r.reset_accumulation()
+        r.draw_next_frame()
+        again = r.read_framebuffer()
+    for f, got in enumerate(outs):
+        want, _ = oracle.render(oracle.config(w, h, (f + 1) * spp, depth, chunk=k,
+                                              frame_spp=spp), scene)
+        assert_bitwise(got, want, f"progressive frame {f}")
+    assert_bitwise(again, outs[0], "after reset")

@@ -139,3 +139,15 @@ def test_tile_partition_is_exact(w, h, world):
     assert len(np.unique(flat)) == w * h
     for r in range(world):
         assert np.all(m[m[..., 0] == r][:, 1] < 64 * counts[r])
+
+
+def test_srgb8_thresholds_agree_with_oracle(oracle):
+    th = np.zeros(255, dtype=np.float32)
+    N.lib().vcrt_srgb8_thresholds(th.ctypes.data)
+    assert np.all(np.diff(th) > 0)
+    # each threshold is the first float the oracle encodes to k; the float below encodes to k-1
+    below = np.nextafter(th, np.float32(-1))
+    px = np.stack([th, below, th, np.ones_like(th)], axis=1)
+    enc = oracle.encode_srgb8(px)
+    assert np.array_equal(enc[:, 0], np.arange(1, 256, dtype=np.uint8))
+    assert np.array_equal(enc[:, 1], np.arange(0, 255, dtype=np.uint8))

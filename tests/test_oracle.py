@@ -158,3 +158,34 @@ def test_chunked_order_is_close_to_sequential(oracle):
     # chunk >= spp is exactly the sequential order
     c, _ = oracle.render(oracle.config(32, 18, 64, 10, chunk=64), oracle.scene("final"))
     assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
+
+
+def _srgb_reference(c):
+    c = np.nan_to_num(np.asarray(c, dtype=np.float64), nan=0.0)
+    c = np.clip(c, 0.0, 1.0)
+    s = np.where(c <= 0.0031308, 12.92 * c, 1.055 * np.power(c, 1 / 2.4) - 0.055)
+    return np.floor(s * 255.0 + 0.5).astype(np.uint8)
+
+
+def test_srgb8_encode_matches_formula(oracle):
+    rng = np.random.default_rng(5)
+    vals = np.concatenate([rng.uniform(-0.1, 1.1, 200000), np.linspace(0, 1, 70001),
+                           [0.0, -0.0, 1.0, 2.0, np.inf, -np.inf, np.nan, 0.0031308, 1e-30]])
+    vals = vals.astype(np.float32)
+    rgba = np.stack([vals, vals[::-1], vals, np.ones_like(vals)], axis=1)
+    got = oracle.encode_srgb8(rgba)
+    want = _srgb_reference(rgba[:, :3].astype(np.float64))
+    assert np.array_equal(got[:, :3], want)
+    assert np.all(got[:, 3] == 255)
+
+
+def test_progressive_frame_blocks(oracle):
+    scene = oracle.scene("three")
+    # frame blocks of 4 with chunk 4 are the same chunks as a plain chunk-4 render
+    a, sa = oracle.render(oracle.config(24, 16, 8, 6, chunk=4, frame_spp=4), scene)
+    b, sb = oracle.render(oracle.config(24, 16, 8, 6, chunk=4), scene)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and sa == sb
+    # frame blocks restart chunks: (3,1),(3,1) differs from (3,3,2) only in summation order
+    c, _ = oracle.render(oracle.config(24, 16, 8, 6, chunk=3, frame_spp=4), scene)
+    d, _ = oracle.render(oracle.config(24, 16, 8, 6, chunk=3), scene)
+    assert np.abs(c.astype(np.float64) - d).max() < 1e-6

@@ -71,6 +71,7 @@ class vcrt_render_desc(ctypes.Structure):
         ("kernel_variant", ctypes.c_int32),
         ("blocks_per_cu", ctypes.c_int32),
         ("accumulate_chunk", ctypes.c_int32),
+        ("progressive", ctypes.c_int32),
         ("code_object_path", ctypes.c_char_p),
     ]
 
@@ -91,6 +92,7 @@ class vcrt_stats(ctypes.Structure):
         ("nspheres", ctypes.c_int32),
         ("lds_bytes", ctypes.c_uint32),
         ("accumulate_chunk", ctypes.c_int32),
+        ("accumulated_spp", ctypes.c_uint64),
         ("debug", ctypes.c_uint64 * 8),
     ]
 
@@ -111,6 +113,9 @@ SIGNATURES = {
     "vcrt_assemble_tiles": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_void_p] +
                             [ctypes.c_int32] * 3 + [ctypes.c_uint32]),
     "vcrt_get_stats": (ctypes.c_int32, [ctypes.POINTER(vcrt_stats)]),
+    "vcrt_reset_accumulation": (ctypes.c_int32, []),
+    "vcrt_read_framebuffer_srgb8": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_size_t]),
+    "vcrt_srgb8_thresholds": (None, [ctypes.c_void_p]),
     "vcrt_shader_load": (ctypes.c_int32, [ctypes.c_char_p]),
     "vcrt_scene_builtin": (ctypes.c_int32,
                            [ctypes.c_int32, ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),

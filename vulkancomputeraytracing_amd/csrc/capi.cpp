@@ -44,7 +44,7 @@ struct RendererState {
     VkPipelineShaderStageCreateInfo stage{};
     hipFunction_t k_trace_lds = nullptr, k_trace_smem = nullptr, k_assemble = nullptr,
                   k_fill = nullptr, k_trace_lds_stats = nullptr, k_trace_smem_stats = nullptr,
-                  k_resolve = nullptr;
+                  k_resolve = nullptr, k_encode = nullptr;
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
     bool debug_stats = false;
     uint32_t work_flags = 0;
@@ -60,6 +60,11 @@ struct RendererState {
     int32_t chunk = 1, nchunks = 1;
     uint32_t total_pixels = 0, total_items = 0;
     float4* d_partial = nullptr;  // [nchunks][total_pixels] chunk sums
+    float4* d_accum = nullptr;    // progressive running sums [total_pixels]
+    uint64_t accumulated = 0;     // samples per pixel accumulated (progressive)
+    std::vector<float2> jitter_host;
+    float* d_srgb_thresholds = nullptr;
+    uchar4* d_srgb = nullptr;
     // per-frame inputs / outputs
     float2* d_jitter = nullptr;
     float4* d_fb_own = nullptr;
@@ -90,6 +95,28 @@ int32_t default_chunk(uint64_t pixels, int32_t spp) {
     while (k > 4 && pixels * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 24))
         k /= 2;
     return k;
+}
+
+// Jitter of sample indices base .. base+n-1 (shader.comp:48 depends only on the index).
+void make_jitter(uint64_t base, int n, std::vector<float2>& out) {
+    out.resize(static_cast<size_t>(n));
+    for (int k = 0; k < n; k++) {
+        const float i = static_cast<float>(base + k), i1 = static_cast<float>(base + k + 1);
+        out[k].x = -0.5f + vcrt::rand2(i, i);
+        out[k].y = -0.5f + vcrt::rand2(i1, i1);
+    }
+}
+
+// sRGB8 thresholds: T_k = the smallest float >= the linear value whose exact sRGB encode is
+// (k - 0.5) / 255, k = 1..255, so that #{k : c >= T_k} is round-to-nearest of 255 * encode(c).
+void srgb_thresholds(float out[255]) {
+    for (int k = 1; k <= 255; k++) {
+        const double s = (k - 0.5) / 255.0;
+        const double lin = s <= 0.04045 ? s / 12.92 : std::pow((s + 0.055) / 1.055, 2.4);
+        float t = static_cast<float>(lin);
+        if (static_cast<double>(t) < lin) t = std::nextafter(t, 2.0f);
+        out[k - 1] = t;
+    }
 }
 
 // 8x8 tiles of a W x H frame owned by `rank` when tile t goes to rank t % world.
@@ -130,6 +157,7 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_assemble, m, "vcrt_assemble"));
     VCRT_TRY(hipModuleGetFunction(&g.k_fill, m, "vcrt_fill"));
     VCRT_TRY(hipModuleGetFunction(&g.k_resolve, m, "vcrt_resolve"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_encode, m, "vcrt_encode_srgb8"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_lds_stats, m, "vcrt_trace_lds_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats"));
     return VK_SUCCESS;
@@ -161,6 +189,7 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (static_cast<int64_t>(d.width) * d.height > (int64_t{1} << 31)) return false;
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
+    if (d.progressive != 0 && d.progressive != 1) return false;
     if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_SMEM) return false;
     return true;
 }
@@ -244,15 +273,19 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
                               [](double x) { return std::tan(x); });
     // Jitter (shader.comp:48) depends only on the sample index: one table per frame config.
     const int spp = g.desc.samples_per_pixel;
-    std::vector<float2> jitter(static_cast<size_t>(spp));
-    for (int i = 0; i < spp; i++) {
-        jitter[i].x = -0.5f + vcrt::rand2(static_cast<float>(i), static_cast<float>(i));
-        jitter[i].y = -0.5f + vcrt::rand2(static_cast<float>(i + 1), static_cast<float>(i + 1));
-    }
+    make_jitter(0, spp, g.jitter_host);
     if ((r = to_vk(hipMalloc(&g.d_jitter, sizeof(float2) * spp))) != VK_SUCCESS) return fail(r);
-    if ((r = to_vk(hipMemcpy(g.d_jitter, jitter.data(), sizeof(float2) * spp,
+    if ((r = to_vk(hipMemcpy(g.d_jitter, g.jitter_host.data(), sizeof(float2) * spp,
                              hipMemcpyHostToDevice))) != VK_SUCCESS)
         return fail(r);
+    {
+        float th[255];
+        srgb_thresholds(th);
+        if ((r = to_vk(hipMalloc(&g.d_srgb_thresholds, sizeof(th)))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemcpy(g.d_srgb_thresholds, th, sizeof(th), hipMemcpyHostToDevice))) !=
+            VK_SUCCESS)
+            return fail(r);
+    }
 
     // Frame sharding: 8x8 tiles, tile t to rank t % world (DESIGN.md "Multi-GPU").
     g.tiles_x = static_cast<uint32_t>((g.desc.width + 7) / 8);
@@ -286,7 +319,12 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         if (items >= (uint64_t{1} << 31)) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
         g.total_items = static_cast<uint32_t>(items);
     }
-    if (g.nchunks > 1 && g.total_pixels) {
+    if (g.desc.progressive && g.total_pixels) {
+        const size_t bytes = sizeof(float4) * g.total_pixels;
+        if ((r = to_vk(hipMalloc(&g.d_accum, bytes))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemset(g.d_accum, 0, bytes))) != VK_SUCCESS) return fail(r);
+    }
+    if ((g.nchunks > 1 || g.desc.progressive) && g.total_pixels) {
         const size_t slab = sizeof(float4) * g.total_pixels * static_cast<size_t>(g.nchunks);
         if ((r = to_vk(hipMalloc(&g.d_partial, slab))) != VK_SUCCESS) return fail(r);
     }
@@ -359,6 +397,8 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     }
     g.nspheres = count;
     g.stats.nspheres = count;
+    g.accumulated = 0;  // a new scene restarts progressive accumulation
+    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, sizeof(float4) * g.total_pixels));
     g.scene_bounded = true;
     for (int32_t i = 0; i < count; i++) {
         const vcrt_sphere& sp = spheres[i];
@@ -382,6 +422,14 @@ vcrt_result vcrt_draw_next_frame(void) {
         const uint32_t grid = std::min<uint32_t>((g.local_elems + 255) / 256, 4096);
         VkResult r = launch(g.k_fill, grid, 256, 0, fp);
         if (r != VK_SUCCESS) return r;
+    }
+    const bool slab = g.nchunks > 1 || g.desc.progressive;
+    if (g.desc.progressive && g.accumulated > 0) {
+        // progressive frames continue the sample sequence: indices accumulated.. (+spp)
+        make_jitter(g.accumulated, g.desc.samples_per_pixel, g.jitter_host);
+        VCRT_TRY(hipMemcpyAsync(g.d_jitter, g.jitter_host.data(),
+                                sizeof(float2) * g.jitter_host.size(), hipMemcpyHostToDevice,
+                                g.stream));
     }
     if (pixels != 0 && g.desc.max_depth > 0) {
         vcrt::TraceParams p{};
@@ -407,7 +455,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.total_items = g.total_items;
         p.chunk = g.chunk;
         p.nchunks = g.nchunks;
-        p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u);
+        p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
+                  (slab ? vcrt::kFlagSlab : 0u);
         const vcrt::f3 v[4] = {g.cam.pixel00, g.cam.delta_u, g.cam.delta_v, g.cam.center};
         for (int i = 0; i < 4; i++) {
             p.cam[3 * i + 0] = v[i].x;
@@ -447,11 +496,12 @@ vcrt_result vcrt_draw_next_frame(void) {
         VkResult r = launch(f, grid, block, lds, p);
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
-        if (g.nchunks > 1) {
-            vcrt::ResolveParams rp{g.d_partial,  g.d_fb,        g.desc.width,
-                                   g.desc.height, g.desc.rank, g.desc.world_size,
-                                   g.tiles_x,     g.local_tiles, g.nchunks,
-                                   g.desc.samples_per_pixel};
+        if (slab) {
+            const float spp_total =
+                static_cast<float>(g.accumulated + static_cast<uint64_t>(g.desc.samples_per_pixel));
+            vcrt::ResolveParams rp{g.d_partial,   g.d_fb,      g.d_accum,     spp_total,
+                                   g.desc.width,  g.desc.height, g.desc.rank, g.desc.world_size,
+                                   g.tiles_x,     g.local_tiles, g.nchunks,   g.desc.samples_per_pixel};
             const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
             r = launch(g.k_resolve, rgrid, 256, 0, rp);
             if (r != VK_SUCCESS) return r;
@@ -464,7 +514,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         float ms = 0.f;
         VCRT_TRY(hipEventElapsedTime(&ms, g.ev_start, g.ev_stop));
         g.stats.kernel_ms = ms;
-        if (g.nchunks > 1) {
+        if (slab) {
             VCRT_TRY(hipEventElapsedTime(&ms, g.ev_stop, g.ev_resolve));
             g.stats.resolve_ms = ms;
         }
@@ -482,6 +532,10 @@ vcrt_result vcrt_draw_next_frame(void) {
     g.stats.samples =
         static_cast<uint64_t>(g.local_pixels) * static_cast<uint64_t>(g.desc.samples_per_pixel);
     g.stats.frames += 1;
+    if (g.desc.progressive && pixels != 0 && g.desc.max_depth > 0)
+        g.accumulated += static_cast<uint64_t>(g.desc.samples_per_pixel);
+    g.stats.accumulated_spp = g.desc.progressive ? g.accumulated
+                                                 : static_cast<uint64_t>(g.desc.samples_per_pixel);
     g.stats.frame_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return VCRT_SUCCESS;
@@ -500,6 +554,9 @@ vcrt_result vcrt_end(void) {
     if (g.ev_stop) (void)hipEventDestroy(g.ev_stop);
     if (g.ev_resolve) (void)hipEventDestroy(g.ev_resolve);
     if (g.d_partial) (void)hipFree(g.d_partial);
+    if (g.d_accum) (void)hipFree(g.d_accum);
+    if (g.d_srgb_thresholds) (void)hipFree(g.d_srgb_thresholds);
+    if (g.d_srgb) (void)hipFree(g.d_srgb);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = RendererState{};
     return VCRT_SUCCESS;
@@ -557,6 +614,36 @@ vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width
     if (r != VK_SUCCESS) return r;
     VCRT_TRY(hipStreamSynchronize(g.stream));
     return VCRT_SUCCESS;
+}
+
+vcrt_result vcrt_reset_accumulation(void) {
+    if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
+    VCRT_TRY(hipStreamSynchronize(g.stream));
+    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, sizeof(float4) * g.total_pixels));
+    g.accumulated = 0;
+    make_jitter(0, g.desc.samples_per_pixel, g.jitter_host);
+    VCRT_TRY(hipMemcpy(g.d_jitter, g.jitter_host.data(), sizeof(float2) * g.jitter_host.size(),
+                       hipMemcpyHostToDevice));
+    return VCRT_SUCCESS;
+}
+
+vcrt_result vcrt_read_framebuffer_srgb8(uint8_t* rgba8, size_t bytes) {
+    if (!g.begun || (!rgba8 && g.local_elems)) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (bytes < static_cast<size_t>(g.local_elems) * 4) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
+    if (!g.local_elems) return VCRT_SUCCESS;
+    if (!g.d_srgb) VCRT_TRY(hipMalloc(&g.d_srgb, sizeof(uchar4) * g.local_elems));
+    vcrt::EncodeParams ep{g.d_fb, g.d_srgb, g.d_srgb_thresholds, g.local_elems};
+    const uint32_t grid = std::min<uint32_t>((g.local_elems + 255) / 256, 4096);
+    VkResult r = launch(g.k_encode, grid, 256, 0, ep);
+    if (r != VK_SUCCESS) return r;
+    VCRT_TRY(hipMemcpyAsync(rgba8, g.d_srgb, sizeof(uchar4) * g.local_elems,
+                            hipMemcpyDeviceToHost, g.stream));
+    VCRT_TRY(hipStreamSynchronize(g.stream));
+    return VCRT_SUCCESS;
+}
+
+void vcrt_srgb8_thresholds(float thresholds[255]) {
+    if (thresholds) srgb_thresholds(thresholds);
 }
 
 vcrt_result vcrt_get_stats(vcrt_stats* stats) {

@@ -333,7 +333,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             acc = add(acc, contrib);
             ++sample;
             if (sample == sample_end) {
-                if (nchunks == 1u)
+                if ((p.flags & kFlagSlab) == 0u)
                     p.out[out_index] =
                         make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
                 else
@@ -394,21 +394,22 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem_stats(TracePar
 
 // Chunk sums -> pixels in chunk order: ((P0 + P1) + P2) + ..., then / spp (shader.comp:56).
 extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) {
-    const float spp_f = (float)p.spp;
     const uint32_t elems = p.local_tiles * 64u;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < elems;
          q += gridDim.x * blockDim.x) {
         const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
                                   (uint32_t)p.world, (uint32_t)p.rank);
         if (!px.valid) continue;
-        float4 s = p.partial[q];
-        for (int c = 1; c < p.nchunks; ++c) {
+        float4 s = p.accum ? p.accum[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c = 0; c < p.nchunks; ++c) {  // 0 + P0 == P0: the first chunk is exact
             const float4 v = p.partial[(size_t)c * elems + q];
             s.x = s.x + v.x;
             s.y = s.y + v.y;
             s.z = s.z + v.z;
         }
-        p.out[px.out_index] = make_float4(s.x / spp_f, s.y / spp_f, s.z / spp_f, 1.0f);
+        if (p.accum) p.accum[q] = s;
+        p.out[px.out_index] =
+            make_float4(s.x / p.spp_total, s.y / p.spp_total, s.z / p.spp_total, 1.0f);
     }
 }
 
@@ -423,6 +424,31 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_assemble(AssembleParams p
         const uint32_t r = t % (uint32_t)p.world, lt = t / (uint32_t)p.world;
         const uint32_t slot = ((y & 7u) << 3) | (x & 7u);
         p.frame[i] = p.gathered[((size_t)r * p.tiles_per_rank + lt) * 64u + slot];
+    }
+}
+
+// sRGB8 encode (present-time conversion of the B8G8R8A8_SRGB swapchain, Frontend.cpp:43):
+// a channel's byte is the number of the 255 host-computed thresholds it reaches, i.e. the
+// round-to-nearest of the exact sRGB encode of the clamped value; alpha is stored linearly.
+extern "C" __global__ __launch_bounds__(256) void vcrt_encode_srgb8(EncodeParams p) {
+    __shared__ float th[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) th[i] = i < 255 ? p.thresholds[i] : 3e38f;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.count;
+         i += gridDim.x * blockDim.x) {
+        const float4 v = p.in[i];
+        const float c[3] = {v.x, v.y, v.z};
+        unsigned char b[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            int lo = 0;  // count of thresholds <= c[k] (NaN reaches none: 0)
+#pragma unroll
+            for (int step = 128; step > 0; step >>= 1)
+                if (c[k] >= th[lo + step - 1]) lo += step;
+            b[k] = (unsigned char)lo;
+        }
+        const float a = v.w != v.w ? 0.0f : fminf(fmaxf(v.w, 0.0f), 1.0f);
+        p.out[i] = make_uchar4(b[0], b[1], b[2], (unsigned char)(a * 255.0f + 0.5f));
     }
 }
 

@@ -43,10 +43,13 @@ struct TraceParams {
 
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
+constexpr uint32_t kFlagSlab = 4u;          // chunk sums always go to the slab (resolve pass)
 
 struct ResolveParams {
     const float4* partial;  // [nchunks][local_tiles * 64]
     float4* out;            // rank-local framebuffer
+    float4* accum;          // progressive running sums [local_tiles * 64], or null
+    float spp_total;        // divisor: samples accumulated so far
     int32_t width, height, rank, world;
     uint32_t tiles_x, local_tiles;
     int32_t nchunks, spp;
@@ -57,6 +60,14 @@ struct AssembleParams {
     float4* frame;           // [height][width]
     int32_t width, height, world;
     uint32_t tiles_x, tiles_per_rank;
+};
+
+// Linear rgba32f -> sRGB8 as the reference's B8G8R8A8_SRGB swapchain stores it (Frontend.cpp:43).
+struct EncodeParams {
+    const float4* in;
+    uchar4* out;
+    const float* thresholds;  // [255] ascending: byte = #{k : c >= thresholds[k]}
+    uint32_t count;
 };
 
 struct FillParams {

@@ -1,8 +1,7 @@
 // vcrt_render -- headless replacement of the reference's main()
 // (VulkanComputeRayTracing.cpp:17-42): Begin -> DrawNextFrame x N -> End, then optionally writes
-// the frame as PFM (linear rgba32f, as the compute image holds it) or PPM (sRGB8, as the
-// B8G8R8A8_SRGB swapchain shows it: Frontend.cpp:43).
-#include <cmath>
+// the frame as PFM (linear rgba32f, as the compute image holds it) or PPM (sRGB8 encoded on the
+// GPU, as the B8G8R8A8_SRGB swapchain shows it: Frontend.cpp:43).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -13,18 +12,10 @@
 
 namespace {
 
-unsigned char srgb8(float linear) {
-    float c = linear;
-    if (!(c > 0.0f)) c = 0.0f;
-    if (c > 1.0f) c = 1.0f;
-    const float s = c <= 0.0031308f ? 12.92f * c : 1.055f * std::pow(c, 1.0f / 2.4f) - 0.055f;
-    return static_cast<unsigned char>(std::lround(s * 255.0f));
-}
-
 int usage() {
     std::fprintf(stderr,
                  "usage: vcrt_render [--width W] [--height H] [--spp N] [--depth D] "
-                 "[--scene final|three|red|stress4096] [--frames F] [--device I] "
+                 "[--scene final|three|red|stress4096] [--frames F] [--progressive 0|1] [--device I] "
                  "[--out file.ppm|file.pfm]\n");
     return 2;
 }
@@ -46,6 +37,7 @@ int main(int argc, char** argv) {
         else if (a == "--depth") desc.max_depth = std::atoi(v);
         else if (a == "--frames") frames = std::atoi(v);
         else if (a == "--device") desc.device = std::atoi(v);
+        else if (a == "--progressive") desc.progressive = std::atoi(v);
         else if (a == "--out") out = v;
         else if (a == "--scene") {
             const std::string s = v;
@@ -75,23 +67,22 @@ int main(int argc, char** argv) {
                     static_cast<unsigned long long>(st.segments));
     }
     if (r == VK_SUCCESS && !out.empty()) {
-        std::vector<float> rgba(static_cast<size_t>(desc.width) * desc.height * 4);
-        r = ReadFramebuffer(rgba.data(), rgba.size());
+        const bool pfm = out.size() > 4 && out.compare(out.size() - 4, 4, ".pfm") == 0;
+        const size_t n = static_cast<size_t>(desc.width) * desc.height;
+        std::vector<float> rgba(pfm ? n * 4 : 0);
+        std::vector<uint8_t> srgb(pfm ? 0 : n * 4);
+        r = pfm ? ReadFramebuffer(rgba.data(), rgba.size())
+                : vcrt_read_framebuffer_srgb8(srgb.data(), srgb.size());  // GPU sRGB encode
         FILE* f = r == VK_SUCCESS ? std::fopen(out.c_str(), "wb") : nullptr;
         if (f) {
-            const bool pfm = out.size() > 4 && out.compare(out.size() - 4, 4, ".pfm") == 0;
             std::fprintf(f, pfm ? "PF\n%d %d\n-1.0\n" : "P6\n%d %d\n255\n", desc.width,
                          desc.height);
             for (int y = pfm ? desc.height - 1 : 0; pfm ? y >= 0 : y < desc.height;
                  y += pfm ? -1 : 1) {
                 for (int x = 0; x < desc.width; x++) {
-                    const float* p = &rgba[(static_cast<size_t>(y) * desc.width + x) * 4];
-                    if (pfm) {
-                        std::fwrite(p, sizeof(float), 3, f);
-                    } else {
-                        const unsigned char c[3] = {srgb8(p[0]), srgb8(p[1]), srgb8(p[2])};
-                        std::fwrite(c, 1, 3, f);
-                    }
+                    const size_t i = static_cast<size_t>(y) * desc.width + x;
+                    if (pfm) std::fwrite(&rgba[4 * i], sizeof(float), 3, f);
+                    else std::fwrite(&srgb[4 * i], 1, 3, f);
                 }
             }
             std::fclose(f);

@@ -33,6 +33,7 @@ class RenderDesc:
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
     accumulate_chunk: int = 0       # 0 = 16; >= spp: the reference's sequential order
+    progressive: bool = False       # frame f continues the sample sequence; average of all frames
     code_object_path: str | None = None
     _path_keepalive: bytes | None = field(default=None, repr=False)
 
@@ -50,6 +51,7 @@ class RenderDesc:
         d.kernel_variant = self.kernel_variant
         d.blocks_per_cu = self.blocks_per_cu
         d.accumulate_chunk = self.accumulate_chunk
+        d.progressive = 1 if self.progressive else 0
         if self.code_object_path:
             self._path_keepalive = self.code_object_path.encode()
             d.code_object_path = self._path_keepalive
@@ -180,6 +182,20 @@ class Renderer:
         N.check("vcrt_read_framebuffer", self._lib.vcrt_read_framebuffer(
             out.ctypes.data_as(ctypes.c_void_p), out.size))
         return out
+
+    def read_framebuffer_srgb8(self) -> np.ndarray:
+        """The rank-local framebuffer as sRGB8 RGBA (what the reference's B8G8R8A8_SRGB
+        swapchain shows), uint8 with the read_framebuffer shape."""
+        elems, tiles = self.local_layout()
+        shape = ((self.desc.height, self.desc.width, 4) if self.desc.world_size == 1
+                 else (tiles, 64, 4))
+        out = np.empty(shape, dtype=np.uint8)
+        N.check("vcrt_read_framebuffer_srgb8", self._lib.vcrt_read_framebuffer_srgb8(
+            out.ctypes.data_as(ctypes.c_void_p), out.size))
+        return out
+
+    def reset_accumulation(self) -> None:
+        N.check("vcrt_reset_accumulation", self._lib.vcrt_reset_accumulation())
 
     def framebuffer_device(self) -> tuple[int, int]:
         p, n = ctypes.c_void_p(), ctypes.c_size_t()
