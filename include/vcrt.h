@@ -68,11 +68,14 @@ typedef struct vcrt_camera { /* globals.glsl:21-24 */
     float vfov; /* degrees */
 } vcrt_camera;
 
-/* Kernel variants. AUTO = SMEM: wave-uniform scalar-cache reads of the sphere table (measured
- * faster than LDS staging for 485 and 4100 spheres). */
+/* Kernel variants. SMEM: wave-uniform scalar-cache reads of the linear sphere table (measured
+ * faster than LDS staging for 485 and 4100 spheres). CULL: spheres grouped
+ * spatially in fours, a group is tested only when some ray of the wave may come near it (same
+ * results bit for bit; falls back to SMEM below 16 spheres or for unbounded scenes). */
 #define VCRT_KERNEL_AUTO 0
 #define VCRT_KERNEL_LDS 1
 #define VCRT_KERNEL_SMEM 2
+#define VCRT_KERNEL_CULL 3
 
 typedef struct vcrt_render_desc {
     uint32_t struct_size;      /* sizeof(vcrt_render_desc) */
@@ -113,6 +116,8 @@ typedef struct vcrt_stats {
     uint32_t lds_bytes;
     int32_t accumulate_chunk; /* samples per work item in effect */
     uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
+    uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
+    uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */
     uint64_t debug[8]; /* diagnostics (VCRT_DEBUG_STATS=1): wave-iterations, active-lane sum,
                           hit groups, fetches, last/first wave end time, sum end time, waves */
 } vcrt_stats;
@@ -167,6 +172,14 @@ int32_t vcrt_scene_builtin(int32_t scene_id, vcrt_sphere* out, int32_t cap);
 /* SceneGenerator stdout, byte for byte. Returns the length (excluding NUL); writes up to cap-1
  * bytes plus NUL when buf != NULL. */
 size_t vcrt_scene_generator_text(char* buf, size_t cap);
+
+/* The CULL variant's grouped tables for a sphere list (host only, no GPU): groups of four in
+ * pair-SoA form (16 floats each), group-pair bounds (16 floats per two groups: Cx0 Cx1 Cy0 Cy1
+ * Cz0 Cz1 R0 R1 Rsq0 Rsq1 Kc0 Kc1 0 0 0 0) and member indices (4 per group, -1 = padding).
+ * Returns the group count (0 = culling does not apply: < 16 spheres or unbounded scene) and
+ * writes the tables when cap_groups is large enough (any pointer may be NULL). */
+int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
+                         int32_t* index, int32_t cap_groups);
 
 /* Canonical math as used by the kernel (host evaluation), for tests and tools. */
 float vcrt_canonical_sin(float x);

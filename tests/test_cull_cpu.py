@@ -1,0 +1,177 @@
+"""CPU checks of the CULL variant's grouped tables (vcrt_cull_tables, csrc/cluster.cpp).
+
+The culled scan is exact only if (1) every sphere sits in exactly one group with the linear
+table's values, and (2) a group whose bound test culls it for a ray holds no sphere whose fp32
+discriminant (hit_sphere, functions.glsl:14-22, as tracer.hip's pair_disc evaluates it) is
+>= 0. (2) is checked here by emulating both fp32 evaluations in numpy on random rays and on
+rays built to graze member spheres within 1e-7..1e-4 of their radius.
+"""
+import numpy as np
+import pytest
+
+from vulkancomputeraytracing_amd import scene as S
+
+f32 = np.float32
+
+
+def fma(x, y, z):
+    # fp32 fma through float64: the product is exact, the sum rounds twice (harmless here)
+    return (x.astype(np.float64) * y.astype(np.float64) + z.astype(np.float64)).astype(f32)
+
+
+def group_culled(t, o, d):
+    """[rays, groups] bool: the kernel's bound test (tracer.hip scan_culled, phase 1)."""
+    b = t["bound"]
+    G = t["geom"].shape[0]
+    cols = lambda k: np.stack([b[:, k], b[:, k + 1]], 1).reshape(G)  # noqa: E731
+    C = [cols(0), cols(2), cols(4)]
+    R, Rsq, Kc = cols(6), cols(8), cols(10)
+    a = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])[:, None]
+    oc = [(o[:, k, None] - C[k][None, :]).astype(f32) for k in range(3)]
+    dd = [np.broadcast_to(d[:, k, None], oc[0].shape) for k in range(3)]
+    oc2 = fma(oc[2], oc[2], fma(oc[1], oc[1], oc[0] * oc[0]))
+    hbc = fma(oc[2], dd[2], fma(oc[1], dd[1], oc[0] * dd[0]))
+    X = fma(-hbc, hbc, a * oc2)
+    RM = fma(np.broadcast_to(Kc, oc2.shape), oc2 + Rsq, np.broadcast_to(R, oc2.shape))
+    a_s = a * f32(f32(1.0) + f32(1e-5))
+    a_e = a * f32(1e-5)
+    thr = fma(np.broadcast_to(a_e, oc2.shape), oc2, a_s * (RM * RM))
+    return X > thr
+
+
+def member_disc(t, o, d):
+    """[rays, groups, 4] fp32 discriminants exactly as pair_disc computes them."""
+    g = t["geom"]
+    cx = np.stack([g[:, 0], g[:, 1], g[:, 8], g[:, 9]], 1)
+    cy = np.stack([g[:, 2], g[:, 3], g[:, 10], g[:, 11]], 1)
+    cz = np.stack([g[:, 4], g[:, 5], g[:, 12], g[:, 13]], 1)
+    r2 = np.stack([g[:, 6], g[:, 7], g[:, 14], g[:, 15]], 1)
+    a = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])[:, None, None]
+    ox, oy, oz = (o[:, k, None, None] for k in range(3))
+    dx, dy, dz = (d[:, k, None, None] for k in range(3))
+    ocx, ocy, ocz = ox - cx[None], oy - cy[None], oz - cz[None]
+    hb = (ocx * dx + ocy * dy) + ocz * dz
+    cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2[None]
+    with np.errstate(over="ignore", invalid="ignore"):  # padding members: r^2 = -3e38
+        return hb * hb - a * cc
+
+
+def grazing_rays(spheres, n, rng):
+    idx = rng.integers(0, len(spheres), n)
+    c = spheres["center"][idx].astype(np.float64)
+    r = np.abs(spheres["radius"][idx].astype(np.float64))
+    dh = rng.normal(size=(n, 3))
+    dh /= np.linalg.norm(dh, axis=1, keepdims=True)
+    p = rng.normal(size=(n, 3))
+    p -= (p * dh).sum(1, keepdims=True) * dh
+    p /= np.linalg.norm(p, axis=1, keepdims=True)
+    delta = rng.choice([-1e-6, 0.0, 1e-7, 3e-7, 1e-6, 1e-5, 1e-4], n)
+    q = c + p * (r * (1 + delta))[:, None]
+    s = rng.uniform(0.5, 40.0, n)[:, None]
+    o = (q - s * dh).astype(f32)
+    d = (dh * rng.choice([0.01, 0.3, 1.0, 7.0, 100.0], n)[:, None]).astype(f32)
+    return o, d
+
+
+def tangent_rays(spheres, t, n, rng):
+    """Rays tangent to a group's bound where its outermost member touches it: they graze the
+    member and the bound at once (the tightest case for the bound test)."""
+    b, G = t["bound"], t["geom"].shape[0]
+    os_, ds_ = [], []
+    for gi in rng.integers(0, G, n):
+        e, bb = gi % 2, b[gi // 2]
+        C = np.array([bb[0 + e], bb[2 + e], bb[4 + e]], np.float64)
+        m = t["index"][gi][t["index"][gi] >= 0]
+        if len(m) == 0:
+            continue
+        c = spheres["center"][m].astype(np.float64)
+        r = np.abs(spheres["radius"][m].astype(np.float64))
+        i = np.argmax(np.linalg.norm(c - C, axis=1) + r)
+        u = c[i] - C
+        u = u / np.linalg.norm(u) if np.linalg.norm(u) > 0 else np.array([0.0, 1.0, 0.0])
+        q = c[i] + u * r[i] * (1 + rng.choice([-1e-6, 0.0, 1e-7, 3e-7, 1e-6, 1e-5]))
+        p = rng.normal(size=3)
+        p -= (p @ u) * u
+        p /= np.linalg.norm(p)
+        os_.append(q - rng.uniform(0.5, 40.0) * p)
+        ds_.append(p * rng.choice([0.01, 1.0, 100.0]))
+    return np.array(os_, f32), np.array(ds_, f32)
+
+
+def random_rays(n, rng, lo, hi):
+    o = rng.uniform(lo, hi, size=(n, 3)).astype(f32)
+    d = (rng.normal(size=(n, 3)) * rng.choice([0.05, 1.0, 20.0], n)[:, None]).astype(f32)
+    return o, d
+
+
+@pytest.mark.parametrize("name", ["final", "stress4096"])
+def test_groups_partition_the_scene(name):
+    sp = S.builtin_scene(name)
+    t = S.cull_tables(sp)
+    assert t is not None
+    G = t["geom"].shape[0]
+    assert G % 2 == 0 and G >= (len(sp) + 3) // 4
+    idx = t["index"].reshape(-1)
+    members = np.sort(idx[idx >= 0])
+    assert np.array_equal(members, np.arange(len(sp)))
+    g = t["geom"]
+    for gi in range(G):
+        for k in range(4):
+            j = t["index"][gi, k]
+            if j < 0:
+                continue
+            base = 8 * (k // 2) + (k % 2)
+            assert g[gi, base] == sp["center"][j, 0]
+            assert g[gi, base + 2] == sp["center"][j, 1]
+            assert g[gi, base + 4] == sp["center"][j, 2]
+            assert g[gi, base + 6] == f32(sp["radius"][j]) * f32(sp["radius"][j])
+            # bound covers the member (float64 geometry)
+            e = gi % 2
+            b = t["bound"][gi // 2]
+            C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
+            dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
+            assert dist + abs(float(sp["radius"][j])) <= float(b[6 + e])
+
+
+def test_small_or_unbounded_scenes_do_not_cull():
+    assert S.cull_tables(S.builtin_scene("three")) is None
+    sp = S.builtin_scene("final").copy()
+    sp["center"][7, 0] = 3e9
+    assert S.cull_tables(sp) is None
+
+
+@pytest.mark.parametrize("name", ["final", "stress4096"])
+def test_bound_test_is_conservative(name):
+    rng = np.random.default_rng(7)
+    sp = S.builtin_scene(name)
+    t = S.cull_tables(sp)
+    valid = t["index"] >= 0
+    total_culled = 0
+    total = 0
+    chunks = [grazing_rays(sp, 1500, rng) for _ in range(3)]
+    chunks += [tangent_rays(sp, t, 1500, rng) for _ in range(2)]
+    chunks += [random_rays(1500, rng, -20.0, 20.0), random_rays(500, rng, -2.0, 2.0)]
+    for o, d in chunks:
+        culled = group_culled(t, o, d)
+        disc = member_disc(t, o, d)
+        hit = (~(disc < 0)) & valid[None]
+        bad = culled[:, :, None] & hit
+        assert not bad.any(), f"{int(bad.sum())} culled group members with disc >= 0"
+        total_culled += int(culled.sum())
+        total += culled.size
+    # and the test does cull (most groups are far from most rays)
+    assert total_culled > 0.5 * total
+
+
+def test_checker_detects_a_too_small_bound():
+    """The emulated check above has teeth: bounds shrunk by 1% are caught."""
+    rng = np.random.default_rng(11)
+    sp = S.builtin_scene("final")
+    t = S.cull_tables(sp)
+    bad_t = {k: v.copy() for k, v in t.items()}
+    bad_t["bound"][:, 6:10] *= f32(0.99)
+    bad_t["bound"][:, 10:12] = 0
+    o, d = tangent_rays(sp, t, 1500, rng)
+    culled = group_culled(bad_t, o, d)
+    hit = ~(member_disc(t, o, d) < 0) & (t["index"] >= 0)[None]
+    assert (culled[:, :, None] & hit).any()

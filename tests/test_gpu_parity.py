@@ -54,7 +54,15 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
+VARIANTS = [vc.KERNEL_LDS, vc.KERNEL_SMEM, vc.KERNEL_CULL]
+
+
+def expected_variant(variant, nspheres):
+    # CULL needs >= 16 spheres (vcrt.h); below that the linear SMEM scan runs
+    return vc.KERNEL_SMEM if variant == vc.KERNEL_CULL and nspheres < 16 else variant
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("scene,w,h,spp,depth", CASES)
 def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     got, st = gpu_render(scene, w, h, spp, depth, variant)
@@ -67,10 +75,10 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     assert got.shape == want.shape
     assert_bitwise(got, want, f"{scene} {w}x{h} spp{spp} d{depth} v{variant}")
     assert st["segments"] == want_segs
-    assert st["kernel_variant"] == variant
+    assert st["kernel_variant"] == expected_variant(variant, st["nspheres"])
 
 
-@pytest.mark.parametrize("variant", [vc.KERNEL_LDS, vc.KERNEL_SMEM])
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("scene,w,h,spp,depth,chunk", [
     ("final", 64, 36, 64, 10, 16),   # 4 chunks
     ("final", 48, 30, 40, 10, 0),    # default chunk for a tiny frame: 4 (10 chunks)
@@ -103,10 +111,53 @@ def test_golden_oracle_images():
 def test_stress_scene_small(oracle):
     w, h, spp, depth = 48, 27, 2, 10
     want, segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("stress4096"))
-    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM):
+    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL):
         got, st = gpu_render("stress4096", w, h, spp, depth, variant)
         assert_bitwise(got, want, f"stress v{variant}")
         assert st["segments"] == segs and st["nspheres"] == 4100
+
+
+def culling_torture_scene():
+    """>= 16 spheres that stress the culled scan's exactness: exact duplicates with different
+    materials (ties must go to the lower index), nested and overlapping spheres, a hollow glass
+    shell (negative radius), spheres below the margin's r_min (1e-3), a huge sphere and a far
+    one."""
+    rng = np.random.default_rng(5)
+    rows = [((0, -1000, 0), 1000.0, (0.5, 0.5, 0.5), 1, 0.0)]
+    for i in range(24):
+        c = (float(rng.uniform(-3, 3)), float(rng.uniform(0.1, 1.5)), float(rng.uniform(-3, 3)))
+        r = float(rng.uniform(0.05, 0.6))
+        rows.append((c, r, tuple(rng.uniform(0, 1, 3)), 1 + i % 3, float(rng.uniform(0, 1.6))))
+        if i % 4 == 0:  # exact duplicate, other material
+            rows.append((c, r, (1.0, 0.0, 0.0), 1 + (i + 1) % 3, 0.3))
+        if i % 6 == 0:  # concentric inner sphere / hollow shell
+            rows.append((c, -0.9 * r, (1, 1, 1), 3, 1.5))
+    rows.append(((0.2, 0.5, 0.1), 5e-4, (0, 1, 0), 1, 0.0))    # tiny: never culled
+    rows.append(((0.2, 0.5, 0.1), 5e-4, (0, 0, 1), 2, 0.0))    # its duplicate
+    rows.append(((0, 4, -2), 3.0, (0.7, 0.6, 0.5), 2, 0.0))
+    rows.append(((40, 3, 90), 2.0, (0.1, 0.8, 0.2), 1, 0.0))
+    return vc.make_spheres(rows)
+
+
+@pytest.mark.parametrize("w,h,spp,depth,chunk", [(64, 40, 8, 12, 0), (33, 21, 5, 50, 5)])
+def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
+    sc = culling_torture_scene()
+    assert len(sc) >= 16
+    cfg = dict(lookfrom=(6, 2.5, 5), lookat=(0, 0.6, 0), vfov=45)
+    k = vc.renderer.effective_chunk(spp, chunk, pixels=vc.tile_slots(w, h))
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
+    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL):
+        desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
+                             device=0, kernel_variant=variant, accumulate_chunk=chunk, **cfg)
+        with vc.Renderer(desc, sc) as r:
+            r.draw_next_frame()
+            got, st = r.read_framebuffer(), r.stats()
+        assert st["kernel_variant"] == variant
+        assert_bitwise(got, want, f"torture v{variant}")
+        assert st["segments"] == segs
+        if variant == vc.KERNEL_CULL:
+            assert 0 < st["group_tests"]
+            assert st["bound_tests"] > 0
 
 
 def test_custom_scene_and_empty_scene(oracle):
@@ -227,10 +278,11 @@ def test_reference_named_lifecycle():
     vc.SetRenderScene(None)
 
 
-def test_full_size_rows_subset_rms(oracle):
+@pytest.mark.parametrize("variant", [vc.KERNEL_AUTO, vc.KERNEL_CULL])
+def test_full_size_rows_subset_rms(oracle, variant):
     # BASELINE config 3 geometry (1920x1080, depth 10) at 16 spp; oracle renders every 90th row.
     w, h, spp, depth = 1920, 1080, 16, 10
-    got, st = gpu_render("final", w, h, spp, depth)
+    got, st = gpu_render("final", w, h, spp, depth, variant)
     rows = range(7, h, 90)
     want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"]),
                             oracle.scene("final"), rows=rows)

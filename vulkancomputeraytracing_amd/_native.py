@@ -32,6 +32,7 @@ TEXTURE_GLASS = 3
 KERNEL_AUTO = 0
 KERNEL_LDS = 1
 KERNEL_SMEM = 2
+KERNEL_CULL = 3
 
 SCENE_FINAL = 0
 SCENE_THREE = 1
@@ -93,6 +94,8 @@ class vcrt_stats(ctypes.Structure):
         ("lds_bytes", ctypes.c_uint32),
         ("accumulate_chunk", ctypes.c_int32),
         ("accumulated_spp", ctypes.c_uint64),
+        ("group_tests", ctypes.c_uint64),
+        ("bound_tests", ctypes.c_uint64),
         ("debug", ctypes.c_uint64 * 8),
     ]
 
@@ -120,6 +123,8 @@ SIGNATURES = {
     "vcrt_scene_builtin": (ctypes.c_int32,
                            [ctypes.c_int32, ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_scene_generator_text": (ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t]),
+    "vcrt_cull_tables": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]),
     "vcrt_canonical_sin": (ctypes.c_float, [ctypes.c_float]),
     "vcrt_canonical_rand": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
     "vcrt_result_string": (ctypes.c_char_p, [ctypes.c_int32]),

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "Shader.hpp"
+#include "cluster.hpp"
 #include "hip_status.hpp"
 #include "scene.hpp"
 #include "vcrt.h"
@@ -30,7 +31,7 @@ namespace {
 
 using vcrt::to_vk;
 
-constexpr size_t kCounterBytes = 256;  // work counter (u32) + segment counter (u64), padded
+constexpr size_t kCounterBytes = 256;  // work (u32), segments (u64), work_done[2] (u64), padded
 constexpr int32_t kDefaultChunk = 16;        // samples per work item (upper end)
 
 struct RendererState {
@@ -44,7 +45,8 @@ struct RendererState {
     VkPipelineShaderStageCreateInfo stage{};
     hipFunction_t k_trace_lds = nullptr, k_trace_smem = nullptr, k_assemble = nullptr,
                   k_fill = nullptr, k_trace_lds_stats = nullptr, k_trace_smem_stats = nullptr,
-                  k_resolve = nullptr, k_encode = nullptr;
+                  k_resolve = nullptr, k_encode = nullptr, k_trace_cull = nullptr,
+                  k_trace_cull_stats = nullptr;
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
     bool debug_stats = false;
     uint32_t work_flags = 0;
@@ -56,6 +58,11 @@ struct RendererState {
     float4* d_center_radius = nullptr;
     float4* d_shade = nullptr;
     float* d_material = nullptr;
+    // culled-scan tables (cluster.hpp); ncgroups == 0 when culling does not apply
+    int32_t ncgroups = 0;
+    float4* d_cgeom = nullptr;
+    float4* d_cbound = nullptr;
+    int4* d_cindex = nullptr;
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
     uint32_t total_pixels = 0, total_items = 0;
@@ -147,6 +154,13 @@ void free_scene() {
     g.d_center_radius = nullptr;
     g.d_shade = nullptr;
     g.d_material = nullptr;
+    if (g.d_cgeom) (void)hipFree(g.d_cgeom);
+    if (g.d_cbound) (void)hipFree(g.d_cbound);
+    if (g.d_cindex) (void)hipFree(g.d_cindex);
+    g.d_cgeom = nullptr;
+    g.d_cbound = nullptr;
+    g.d_cindex = nullptr;
+    g.ncgroups = 0;
     g.nspheres = 0;
 }
 
@@ -160,6 +174,8 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_encode, m, "vcrt_encode_srgb8"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_lds_stats, m, "vcrt_trace_lds_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull, m, "vcrt_trace_cull"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_stats, m, "vcrt_trace_cull_stats"));
     return VK_SUCCESS;
 }
 
@@ -190,7 +206,7 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
     if (d.progressive != 0 && d.progressive != 1) return false;
-    if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_SMEM) return false;
+    if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL) return false;
     return true;
 }
 
@@ -379,8 +395,22 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         shade[i] = make_float4(sp.colour[0], sp.colour[1], sp.colour[2], sp.texture[1]);
         mat[i] = sp.texture[0];
     }
+    vcrt::CullTables ct;
+    vcrt::build_cull_tables(spheres, count, ct);
     (void)hipStreamSynchronize(g.stream);
     free_scene();
+    if (ct.ngroups > 0) {
+        VCRT_TRY(hipMalloc(&g.d_cgeom, sizeof(float) * ct.geom.size()));
+        VCRT_TRY(hipMalloc(&g.d_cbound, sizeof(float) * ct.bound.size()));
+        VCRT_TRY(hipMalloc(&g.d_cindex, sizeof(int32_t) * ct.index.size()));
+        VCRT_TRY(hipMemcpy(g.d_cgeom, ct.geom.data(), sizeof(float) * ct.geom.size(),
+                           hipMemcpyHostToDevice));
+        VCRT_TRY(hipMemcpy(g.d_cbound, ct.bound.data(), sizeof(float) * ct.bound.size(),
+                           hipMemcpyHostToDevice));
+        VCRT_TRY(hipMemcpy(g.d_cindex, ct.index.data(), sizeof(int32_t) * ct.index.size(),
+                           hipMemcpyHostToDevice));
+        g.ncgroups = ct.ngroups;
+    }
     VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float) * table.size()));
     VCRT_TRY(hipMemcpy(g.d_geom, table.data(), sizeof(float) * table.size(),
                        hipMemcpyHostToDevice));
@@ -443,6 +473,11 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.work = static_cast<uint32_t*>(g.d_counters);
         p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
         p.debug = static_cast<unsigned long long*>(g.d_debug);
+        p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);
+        p.cgeom = g.d_cgeom;
+        p.cbound = g.d_cbound;
+        p.cindex = g.d_cindex;
+        p.ncgroups = g.ncgroups;
         p.nspheres = g.nspheres;
         p.width = g.desc.width;
         p.height = g.desc.height;
@@ -472,9 +507,14 @@ vcrt_result vcrt_draw_next_frame(void) {
         // from L2 behind the one-group prefetch), so AUTO always picks it.
         if (variant == VCRT_KERNEL_AUTO) variant = VCRT_KERNEL_SMEM;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
-        hipFunction_t f = variant == VCRT_KERNEL_LDS ? g.k_trace_lds : g.k_trace_smem;
+        if (variant == VCRT_KERNEL_CULL && g.ncgroups == 0) variant = VCRT_KERNEL_SMEM;
+        hipFunction_t f = variant == VCRT_KERNEL_LDS    ? g.k_trace_lds
+                          : variant == VCRT_KERNEL_CULL ? g.k_trace_cull
+                                                        : g.k_trace_smem;
         if (g.debug_stats)
-            f = variant == VCRT_KERNEL_LDS ? g.k_trace_lds_stats : g.k_trace_smem_stats;
+            f = variant == VCRT_KERNEL_LDS    ? g.k_trace_lds_stats
+                : variant == VCRT_KERNEL_CULL ? g.k_trace_cull_stats
+                                              : g.k_trace_smem_stats;
         const uint32_t lds = variant == VCRT_KERNEL_LDS ? geom_lds : 0;
         const uint32_t block = 256;
         int per_cu = g.desc.blocks_per_cu;
@@ -507,7 +547,7 @@ vcrt_result vcrt_draw_next_frame(void) {
             if (r != VK_SUCCESS) return r;
             VCRT_TRY(hipEventRecord(g.ev_resolve, g.stream));
         }
-        unsigned long long counters[2] = {0, 0};
+        unsigned long long counters[4] = {0, 0, 0, 0};
         VCRT_TRY(hipMemcpyAsync(counters, g.d_counters, sizeof(counters), hipMemcpyDeviceToHost,
                                 g.stream));
         VCRT_TRY(hipStreamSynchronize(g.stream));
@@ -519,6 +559,8 @@ vcrt_result vcrt_draw_next_frame(void) {
             g.stats.resolve_ms = ms;
         }
         g.stats.segments = counters[1];
+        g.stats.group_tests = counters[2];
+        g.stats.bound_tests = counters[3];
         if (g.debug_stats)
             VCRT_TRY(hipMemcpy(g.stats.debug, g.d_debug, sizeof(g.stats.debug),
                                hipMemcpyDeviceToHost));
@@ -677,6 +719,19 @@ size_t vcrt_scene_generator_text(char* buf, size_t cap) {
         buf[k] = '\0';
     }
     return t.size();
+}
+
+int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
+                         int32_t* index, int32_t cap_groups) {
+    if (count < 0 || (count > 0 && !spheres)) return 0;
+    vcrt::CullTables ct;
+    if (!vcrt::build_cull_tables(spheres, count, ct)) return 0;
+    if (ct.ngroups <= cap_groups) {
+        if (geom) std::memcpy(geom, ct.geom.data(), sizeof(float) * ct.geom.size());
+        if (bound) std::memcpy(bound, ct.bound.data(), sizeof(float) * ct.bound.size());
+        if (index) std::memcpy(index, ct.index.data(), sizeof(int32_t) * ct.index.size());
+    }
+    return ct.ngroups;
 }
 
 float vcrt_canonical_sin(float x) { return vcrt::sin_canonical(x); }

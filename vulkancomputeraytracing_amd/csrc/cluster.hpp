@@ -1,0 +1,27 @@
+// cluster.hpp -- spatial grouping of the sphere list for the culled scan (variant CULL).
+//
+// The reference scans world[] linearly for every ray (functions.glsl:77-81). Because that scan
+// picks the smallest accepted t with ties to the earliest index (tracer.hip, scan_culled), the
+// spheres can be visited in any order; this module reorders them into spatially compact groups
+// of four with conservative bounding spheres so a wave can skip groups no lane's ray comes near.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "vcrt.h"
+
+namespace vcrt {
+
+struct CullTables {
+    int32_t ngroups = 0;          // even (a dummy group pads an odd count)
+    std::vector<float> geom;      // [ngroups][16] pair-SoA, same values as the linear table
+    std::vector<float> bound;     // [ngroups / 2][16] group-pair bounds (see TraceParams.cbound)
+    std::vector<int32_t> index;   // [ngroups][4] world[] index of each member, -1 = padding
+};
+
+// Builds the grouped tables. Returns false (tables empty) when culling does not apply: fewer
+// than 16 spheres or any centre/radius outside +-2^30 (or not finite).
+bool build_cull_tables(const vcrt_sphere* spheres, int32_t count, CullTables& out);
+
+}  // namespace vcrt

@@ -166,6 +166,90 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Culled scan (variant CULL). Exact under two facts, both for finite rays (finite_ok, ray_ok):
+//  (1) hit_sphere's sequential scan with strict < (functions.glsl:27-29,77-81) selects the
+//      candidate with the smallest t, earliest index on ties, where t = root1 if root1 > min_t
+//      else root2, kept if min_t < t < 1e5 -- so spheres may be visited in any order;
+//  (2) a group whose bounding sphere (C, R) no ray line of the wave comes within R + M of
+//      contains no sphere whose exact fp32 discriminant is >= 0. With u = 2^-24 the computed
+//      discriminant differs from a*(r^2 - dist^2) by at most ~17u*a*(|oc|^2 + r^2) (rounded oc,
+//      hb, a, cc, products, differences), so dist > r + g*|oc|^2/r with g = 17u implies disc < 0;
+//      M = Kc*(|oC|^2 + R^2) with Kc = 2*8*17u / r_min keeps an 8x safety factor (|oc| <= |oC| +
+//      R, (x+y)^2 <= 2x^2 + 2y^2), and the fp32 evaluation of the group test itself carries a
+//      1e-5 relative slack that covers its own rounding.
+// Waves holding a ray outside the guarded range scan the original table in reference order.
+
+// t of one candidate as hit_sphere would accept it (finite case, fact (1)).
+__device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
+    const float sq = __builtin_sqrtf(disc);
+    const float r1 = (-hb - sq) / a;
+    if (r1 > 0.001f) return r1;
+    return (-hb + sq) / a;
+}
+
+__device__ __forceinline__ void consider(float t, int idx, float& max_t, int& best) {
+    if (t > 0.001f && (t < max_t || (t == max_t && best >= 0 && idx < best))) {
+        max_t = t;
+        best = idx;
+    }
+}
+
+__device__ __forceinline__ v2f vfma(v2f x, v2f y, v2f z) { return __builtin_elementwise_fma(x, y, z); }
+
+__device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, const f3 d,
+                                            float& max_t, int& best, uint64_t& groups_tested,
+                                            uint64_t& bounds_tested) {
+    const float a = dot(d, d);
+    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
+    const v2f a2s = a2 * (v2f){1.0f + 1e-5f, 1.0f + 1e-5f};  // group-test slack
+    const v2f a2e = a2 * (v2f){1e-5f, 1e-5f};
+    cfloat4* bound = (cfloat4*)p.cbound;
+    cfloat4* geom = (cfloat4*)p.cgeom;
+    const int ncg = p.ncgroups;
+    for (int base = 0; base < ncg; base += 64) {
+        // phase 1: which of the next 64 groups can any lane of the wave hit?
+        uint64_t need = 0;
+        const int cnt = min(64, ncg - base);
+        for (int k = 0; k < cnt; k += 2) {
+            const int bp = (base + k) >> 1;
+            const float4 b0 = bound[4 * bp], b1 = bound[4 * bp + 1], b2 = bound[4 * bp + 2];
+            const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y}, R = {b1.z, b1.w};
+            const v2f Rsq = {b2.x, b2.y}, Kc = {b2.z, b2.w};
+            const v2f ocx = ox - Cx, ocy = oy - Cy, ocz = oz - Cz;
+            const v2f oc2 = vfma(ocz, ocz, vfma(ocy, ocy, ocx * ocx));
+            const v2f hbc = vfma(ocz, dz, vfma(ocy, dy, ocx * dx));
+            const v2f X = vfma(-hbc, hbc, a2 * oc2);           // ~ a * dist^2
+            const v2f RM = vfma(Kc, oc2 + Rsq, R);             // R + M
+            const v2f thr = vfma(a2e, oc2, a2s * (RM * RM));   // ~ a * (R + M)^2 + slack
+            if (__ballot(!(X.x > thr.x))) need |= 1ull << k;
+            if (__ballot(!(X.y > thr.y))) need |= 2ull << k;
+        }
+        bounds_tested += (uint64_t)cnt;
+        // phase 2: the exact hit_sphere test on the groups that survived
+        while (need) {
+            const int k = __builtin_ctzll(need);
+            need &= need - 1;
+            const int gi = base + k;
+            ++groups_tested;
+            const float4 q0 = geom[4 * gi], q1 = geom[4 * gi + 1], q2 = geom[4 * gi + 2],
+                         q3 = geom[4 * gi + 3];
+            v2f hb01, d01, hb23, d23;
+            pair_disc(ox, oy, oz, dx, dy, dz, a2, q0, q1, hb01, d01);
+            pair_disc(ox, oy, oz, dx, dy, dz, a2, q2, q3, hb23, d23);
+            const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
+            if (__ballot(!(m4 < 0.0f))) {
+                const int4 id = ((__attribute__((address_space(4))) const int4*)p.cindex)[gi];
+                if (!(d01.x < 0.0f) && id.x >= 0) consider(candidate_t(hb01.x, d01.x, a), id.x, max_t, best);
+                if (!(d01.y < 0.0f) && id.y >= 0) consider(candidate_t(hb01.y, d01.y, a), id.y, max_t, best);
+                if (!(d23.x < 0.0f) && id.z >= 0) consider(candidate_t(hb23.x, d23.x, a), id.z, max_t, best);
+                if (!(d23.y < 0.0f) && id.w >= 0) consider(candidate_t(hb23.y, d23.y, a), id.w, max_t, best);
+            }
+        }
+    }
+}
+
 // Local element q = 64 * lt + slot of this rank -> pixel (x, y) and its framebuffer index.
 struct Pixel {
     uint32_t x, y, out_index;
@@ -185,7 +269,7 @@ __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, ui
     return px;
 }
 
-template <bool kLds, bool kStats>
+template <bool kLds, bool kStats, bool kCull = false>
 __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geom) {
     const int n = p.nspheres;
     if constexpr (kLds) {
@@ -208,6 +292,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     f3 pc = mk(0.f, 0.f, 0.f), o = pc, d = pc, atten = pc, acc = pc;
     unsigned long long segs = 0;
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
+    uint64_t w_groups = 0, w_bounds = 0;  // per wave (uniform): sphere groups / bounds tested
 
     for (;;) {
         // ---- lanes whose item is finished take the next ones (one atomic per wave) ----
@@ -264,7 +349,22 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         float max_t = 1e5f;
         int best = -1;
         uint32_t hit_groups = 0;
-        scan_spheres<kLds>(p, lds_geom, n, o, d, max_t, best, hit_groups);
+        if constexpr (kCull) {
+            // culling needs every ray of the wave in the guarded finite range (see above)
+            const float aa = dot(d, d);
+            const bool guarded = (p.flags & kFlagSceneBounded) != 0 && aa >= 0x1p-20f &&
+                                 aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
+                                 fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
+            if (__ballot(!guarded) == 0) {
+                scan_culled(p, o, d, max_t, best, w_groups, w_bounds);
+            } else {
+                scan_spheres<false>(p, lds_geom, n, o, d, max_t, best, hit_groups);
+                w_groups += (uint64_t)((n + 3) >> 2);
+            }
+        } else {
+            scan_spheres<kLds>(p, lds_geom, n, o, d, max_t, best, hit_groups);
+            w_groups += (uint64_t)((n + 3) >> 2);
+        }
         if constexpr (kStats) st_hitgroups += hit_groups;
 
         // ---- shade (textures.glsl) or sky (functions.glsl:85-89) ----
@@ -356,6 +456,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
     if (lane == 0 && total) atomicAdd(p.segments, total);
+    if (lane == 0 && p.work_done) {
+        atomicAdd(p.work_done + 0, (unsigned long long)w_groups);
+        atomicAdd(p.work_done + 1, (unsigned long long)w_bounds);
+    }
     if constexpr (kStats) {
         if (lane == 0 && p.debug) {
             atomicAdd(p.debug + 0, (unsigned long long)st_iters);
@@ -380,6 +484,15 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_lds(TraceParams p) 
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem(TraceParams p) {
     trace_impl<false, false>(p, nullptr);
+}
+
+// Culled scan (exact; see scan_culled): spatially grouped sphere table + wave-level group tests.
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull(TraceParams p) {
+    trace_impl<false, false, true>(p, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_stats(TraceParams p) {
+    trace_impl<false, true, true>(p, nullptr);
 }
 
 // Diagnostics builds (VCRT_DEBUG_STATS=1): same kernels plus lane-occupancy/tail counters.

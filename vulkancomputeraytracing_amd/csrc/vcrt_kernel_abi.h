@@ -29,6 +29,13 @@ struct TraceParams {
     uint32_t* work;        // work-item counter, zeroed before every launch
     unsigned long long* segments;  // ray segments traced, zeroed before every launch
     unsigned long long* debug;     // diagnostics counters (stats kernels only), may be null
+    unsigned long long* work_done;  // [2]: sphere groups tested, group bounds tested
+    // spatially clustered copy of the scene for the culled scan (kernel variant CULL)
+    const float4* cgeom;    // [ncgroups * 4 + 4] pair-SoA groups of four, spatial order
+    const float4* cbound;   // [ncgroups / 2 * 4] bounds of group pairs, pair-SoA:
+                            //   (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,R0,R1) (Rsq0,Rsq1,Kc0,Kc1) (0,0,0,0)
+    const int4* cindex;     // [ncgroups] world[] index of each member, -1 = padding
+    int32_t ncgroups;       // even
     int32_t nspheres;
     int32_t width, height, spp, max_depth;
     int32_t rank, world;
