@@ -19,24 +19,29 @@ def fma(x, y, z):
     return (x.astype(np.float64) * y.astype(np.float64) + z.astype(np.float64)).astype(f32)
 
 
-def group_culled(t, o, d):
-    """[rays, groups] bool: the kernel's bound test (tracer.hip scan_culled, phase 1)."""
-    b = t["bound"]
-    G = t["geom"].shape[0]
+def group_culled(t, o, d, key="bound", rng=None):
+    """[rays, bounds] bool: the kernel's bound test (tracer.hip bound_pair_need) on the group
+    bounds (key "bound") or the node bounds ("node"). v_rsq_f32's error (~1 ulp) is emulated
+    by a random +-2 ulp perturbation of the exact reciprocal square root."""
+    b = t[key]
+    G = 2 * b.shape[0]
     cols = lambda k: np.stack([b[:, k], b[:, k + 1]], 1).reshape(G)  # noqa: E731
     C = [cols(0), cols(2), cols(4)]
-    R, Rsq, Kc = cols(6), cols(8), cols(10)
-    a = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])[:, None]
+    K, Rk = cols(6), cols(8)
+    a = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
+    inv = (1.0 / np.sqrt(a.astype(np.float64))).astype(f32)
+    if rng is not None:
+        inv = (inv * (1 + rng.uniform(-2.4e-7, 2.4e-7, inv.shape))).astype(f32)
+    w = (d * inv[:, None]).astype(f32)
     oc = [(o[:, k, None] - C[k][None, :]).astype(f32) for k in range(3)]
-    dd = [np.broadcast_to(d[:, k, None], oc[0].shape) for k in range(3)]
+    ww = [np.broadcast_to(w[:, k, None], oc[0].shape) for k in range(3)]
     oc2 = fma(oc[2], oc[2], fma(oc[1], oc[1], oc[0] * oc[0]))
-    hbc = fma(oc[2], dd[2], fma(oc[1], dd[1], oc[0] * dd[0]))
-    X = fma(-hbc, hbc, a * oc2)
-    RM = fma(np.broadcast_to(Kc, oc2.shape), oc2 + Rsq, np.broadcast_to(R, oc2.shape))
-    a_s = a * f32(f32(1.0) + f32(1e-5))
-    a_e = a * f32(1e-5)
-    thr = fma(np.broadcast_to(a_e, oc2.shape), oc2, a_s * (RM * RM))
-    return X > thr
+    h = fma(oc[2], ww[2], fma(oc[1], ww[1], oc[0] * ww[0]))
+    X = fma(-h, h, oc2)
+    with np.errstate(invalid="ignore", over="ignore"):
+        RM = fma(np.broadcast_to(K, oc2.shape), oc2, np.broadcast_to(Rk, oc2.shape))
+        T = RM * RM
+        return X > T
 
 
 def member_disc(t, o, d):
@@ -73,14 +78,19 @@ def grazing_rays(spheres, n, rng):
     return o, d
 
 
+def bound_of(t, gi):
+    e, bb = gi % 2, t["bound"][gi // 2]
+    return np.array([bb[0 + e], bb[2 + e], bb[4 + e]], np.float64)
+
+
 def tangent_rays(spheres, t, n, rng):
-    """Rays tangent to a group's bound where its outermost member touches it: they graze the
-    member and the bound at once (the tightest case for the bound test)."""
-    b, G = t["bound"], t["geom"].shape[0]
+    """Rays tangent to a group's outermost member on the side facing away from the group
+    centre: they graze the member where it touches the bounding sphere (the tightest case for
+    the bound test)."""
+    G = t["geom"].shape[0]
     os_, ds_ = [], []
     for gi in rng.integers(0, G, n):
-        e, bb = gi % 2, b[gi // 2]
-        C = np.array([bb[0 + e], bb[2 + e], bb[4 + e]], np.float64)
+        C = bound_of(t, gi)
         m = t["index"][gi][t["index"][gi] >= 0]
         if len(m) == 0:
             continue
@@ -110,7 +120,7 @@ def test_groups_partition_the_scene(name):
     t = S.cull_tables(sp)
     assert t is not None
     G = t["geom"].shape[0]
-    assert G % 2 == 0 and G >= (len(sp) + 3) // 4
+    assert G % 16 == 0 and G >= (len(sp) + 3) // 4 and t["node"].shape[0] == G // 16
     idx = t["index"].reshape(-1)
     members = np.sort(idx[idx >= 0])
     assert np.array_equal(members, np.arange(len(sp)))
@@ -125,12 +135,18 @@ def test_groups_partition_the_scene(name):
             assert g[gi, base + 2] == sp["center"][j, 1]
             assert g[gi, base + 4] == sp["center"][j, 2]
             assert g[gi, base + 6] == f32(sp["radius"][j]) * f32(sp["radius"][j])
-            # bound covers the member (float64 geometry)
+            # bound covers the member: Rk >= R (float64 geometry)
             e = gi % 2
             b = t["bound"][gi // 2]
             C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
             dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
-            assert dist + abs(float(sp["radius"][j])) <= float(b[6 + e])
+            assert dist + abs(float(sp["radius"][j])) <= float(b[8 + e])
+            # and so does its node's
+            ni = gi // 8
+            e, b = ni % 2, t["node"][ni // 2]
+            C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
+            dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
+            assert dist + abs(float(sp["radius"][j])) <= float(b[8 + e])
 
 
 def test_small_or_unbounded_scenes_do_not_cull():
@@ -152,11 +168,15 @@ def test_bound_test_is_conservative(name):
     chunks += [tangent_rays(sp, t, 1500, rng) for _ in range(2)]
     chunks += [random_rays(1500, rng, -20.0, 20.0), random_rays(500, rng, -2.0, 2.0)]
     for o, d in chunks:
-        culled = group_culled(t, o, d)
+        culled = group_culled(t, o, d, rng=rng)
         disc = member_disc(t, o, d)
         hit = (~(disc < 0)) & valid[None]
         bad = culled[:, :, None] & hit
         assert not bad.any(), f"{int(bad.sum())} culled group members with disc >= 0"
+        # a culled node (8 consecutive groups) holds no hit either
+        node_culled = np.repeat(group_culled(t, o, d, "node", rng=rng), 8, axis=1)
+        bad = node_culled[:, :, None] & hit
+        assert not bad.any(), f"{int(bad.sum())} culled node members with disc >= 0"
         total_culled += int(culled.sum())
         total += culled.size
     # and the test does cull (most groups are far from most rays)
@@ -169,9 +189,28 @@ def test_checker_detects_a_too_small_bound():
     sp = S.builtin_scene("final")
     t = S.cull_tables(sp)
     bad_t = {k: v.copy() for k, v in t.items()}
-    bad_t["bound"][:, 6:10] *= f32(0.99)
-    bad_t["bound"][:, 10:12] = 0
+    bad_t["bound"][:, 6:8] = 0                   # no margin
+    bad_t["bound"][:, 8:10] *= f32(0.99)         # radius 1% short
     o, d = tangent_rays(sp, t, 1500, rng)
     culled = group_culled(bad_t, o, d)
     hit = ~(member_disc(t, o, d) < 0) & (t["index"] >= 0)[None]
     assert (culled[:, :, None] & hit).any()
+
+
+def test_margin_constants():
+    """K and Rk as tracer.hip derives them: K >= 32.4u / r_min (1 + 1e-5) + 6e-6 / (2R) and
+    Rk >= (R + 1.5 Kc R^2)(1 + 1e-5) with R the covering radius."""
+    sp = S.builtin_scene("final")
+    t = S.cull_tables(sp)
+    u = 2.0 ** -24
+    for gi in range(t["geom"].shape[0]):
+        m = t["index"][gi][t["index"][gi] >= 0]
+        if len(m) == 0:
+            continue
+        e, bb = gi % 2, t["bound"][gi // 2]
+        C = bound_of(t, gi)
+        r = np.abs(sp["radius"][m].astype(np.float64))
+        R = (np.linalg.norm(sp["center"][m].astype(np.float64) - C, axis=1) + r).max()
+        Kc = 32.4 * u / r.min()
+        assert float(bb[6 + e]) >= Kc * (1 + 1e-5) + 6e-6 / (2 * R * (1 + 1e-6))
+        assert float(bb[8 + e]) >= (R + 1.5 * Kc * R * R) * (1 + 1e-5)

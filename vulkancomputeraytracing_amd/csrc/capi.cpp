@@ -62,6 +62,7 @@ struct RendererState {
     int32_t ncgroups = 0;
     float4* d_cgeom = nullptr;
     float4* d_cbound = nullptr;
+    float4* d_cnode = nullptr;
     int4* d_cindex = nullptr;
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
@@ -156,9 +157,11 @@ void free_scene() {
     g.d_material = nullptr;
     if (g.d_cgeom) (void)hipFree(g.d_cgeom);
     if (g.d_cbound) (void)hipFree(g.d_cbound);
+    if (g.d_cnode) (void)hipFree(g.d_cnode);
     if (g.d_cindex) (void)hipFree(g.d_cindex);
     g.d_cgeom = nullptr;
     g.d_cbound = nullptr;
+    g.d_cnode = nullptr;
     g.d_cindex = nullptr;
     g.ncgroups = 0;
     g.nspheres = 0;
@@ -402,7 +405,10 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     if (ct.ngroups > 0) {
         VCRT_TRY(hipMalloc(&g.d_cgeom, sizeof(float) * ct.geom.size()));
         VCRT_TRY(hipMalloc(&g.d_cbound, sizeof(float) * ct.bound.size()));
+        VCRT_TRY(hipMalloc(&g.d_cnode, sizeof(float) * ct.node.size()));
         VCRT_TRY(hipMalloc(&g.d_cindex, sizeof(int32_t) * ct.index.size()));
+        VCRT_TRY(hipMemcpy(g.d_cnode, ct.node.data(), sizeof(float) * ct.node.size(),
+                           hipMemcpyHostToDevice));
         VCRT_TRY(hipMemcpy(g.d_cgeom, ct.geom.data(), sizeof(float) * ct.geom.size(),
                            hipMemcpyHostToDevice));
         VCRT_TRY(hipMemcpy(g.d_cbound, ct.bound.data(), sizeof(float) * ct.bound.size(),
@@ -476,6 +482,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);
         p.cgeom = g.d_cgeom;
         p.cbound = g.d_cbound;
+        p.cnode = g.d_cnode;
         p.cindex = g.d_cindex;
         p.ncgroups = g.ncgroups;
         p.nspheres = g.nspheres;
@@ -722,13 +729,14 @@ size_t vcrt_scene_generator_text(char* buf, size_t cap) {
 }
 
 int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
-                         int32_t* index, int32_t cap_groups) {
+                         float* node, int32_t* index, int32_t cap_groups) {
     if (count < 0 || (count > 0 && !spheres)) return 0;
     vcrt::CullTables ct;
     if (!vcrt::build_cull_tables(spheres, count, ct)) return 0;
     if (ct.ngroups <= cap_groups) {
         if (geom) std::memcpy(geom, ct.geom.data(), sizeof(float) * ct.geom.size());
         if (bound) std::memcpy(bound, ct.bound.data(), sizeof(float) * ct.bound.size());
+        if (node) std::memcpy(node, ct.node.data(), sizeof(float) * ct.node.size());
         if (index) std::memcpy(index, ct.index.data(), sizeof(int32_t) * ct.index.size());
     }
     return ct.ngroups;

@@ -53,6 +53,72 @@ void split(std::vector<int32_t>& idx, size_t lo, size_t hi, const vcrt_sphere* s
     split(idx, mid, hi, s, groups);
 }
 
+constexpr double kU = 0x1p-24;           // fp32 unit roundoff
+constexpr double kKcNum = 32.4 * kU;       // Kc = kKcNum / r_min (tracer.hip, (2))
+constexpr double kRel = 1e-5;              // relative slack of the bound test
+constexpr double kAbs = 6e-6;              // evaluation slack * |oC|^2 (> 35u)
+
+struct Bound {
+    float C[3] = {3.0e8f, 3.0e8f, 3.0e8f};  // padding: far away, zero size (K = Rk = 0)
+    float K = 0.f, Rk = 0.f;                // the lane test: RM = K |oC|^2 + Rk
+};
+
+// Bound of `members`: centre of their box (rounded to fp32 first), radius R covering every
+// member from that fp32 centre (+1e-6 relative), margin Kc = 32.4u / r_min, and the kernel's
+// constants K = Kc (1 + 1e-5) + 6e-6 / (2R), Rk = (R + 1.5 Kc R^2)(1 + 1e-5), rounded up
+// (tracer.hip). r_min < 1e-3: K = inf, never culled. No members (padding): a zero-size bound
+// far away, culled by every ray not aimed straight at it (harmless: its groups are empty).
+Bound bound_of(const vcrt_sphere* s, const std::vector<int32_t>& members) {
+    Bound b;
+    if (members.empty()) return b;
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; a++) {
+        lo[a] = std::numeric_limits<double>::infinity();
+        hi[a] = -lo[a];
+    }
+    double rmin = std::numeric_limits<double>::infinity();
+    for (int32_t j : members) {
+        const double r = std::fabs(static_cast<double>(s[j].radius));
+        rmin = std::min(rmin, r);
+        for (int a = 0; a < 3; a++) {
+            lo[a] = std::min(lo[a], s[j].center[a] - r);
+            hi[a] = std::max(hi[a], s[j].center[a] + r);
+        }
+    }
+    for (int a = 0; a < 3; a++) b.C[a] = static_cast<float>(0.5 * (lo[a] + hi[a]));
+    double rad = 0.0;
+    for (int32_t j : members) {
+        double d2 = 0.0;
+        for (int a = 0; a < 3; a++) {
+            const double d = static_cast<double>(s[j].center[a]) - b.C[a];
+            d2 += d * d;
+        }
+        rad = std::max(rad, std::sqrt(d2) + std::fabs(static_cast<double>(s[j].radius)));
+    }
+    const double R = std::max(rad * (1.0 + 1e-6), 1e-30);
+    if (rmin < 1e-3) {
+        b.K = std::numeric_limits<float>::infinity();
+        b.Rk = round_up(R);
+        return b;
+    }
+    const double Kc = kKcNum / rmin;
+    b.K = round_up(Kc * (1.0 + kRel) + kAbs / (2.0 * R));
+    b.Rk = round_up((R + 1.5 * Kc * R * R) * (1.0 + kRel));
+    return b;
+}
+
+// Element i of a pair-SoA bound table (TraceParams.cbound):
+//   (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1) (Rk0,Rk1,0,0)
+void put_bound(std::vector<float>& table, size_t i, const Bound& b) {
+    float* t = &table[(i / 2) * 12];
+    const int e = i % 2;
+    t[0 + e] = b.C[0];
+    t[2 + e] = b.C[1];
+    t[4 + e] = b.C[2];
+    t[6 + e] = b.K;
+    t[8 + e] = b.Rk;
+}
+
 }  // namespace
 
 bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
@@ -70,16 +136,20 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
     const float huge = 8.0f * sorted[count / 2];
     std::vector<int32_t> normal, big;
     for (int32_t i = 0; i < count; i++) (radii[i] > huge ? big : normal).push_back(i);
+    // Big spheres first, in groups of their own.
     std::vector<Group> groups;
-    if (!normal.empty()) split(normal, 0, normal.size(), s, groups);
     if (!big.empty()) split(big, 0, big.size(), s, groups);
-    if (groups.size() % 2) groups.push_back(Group{-1, -1, -1, -1});
+    if (!normal.empty()) split(normal, 0, normal.size(), s, groups);
+    // pad to whole nodes of kNodeGroups groups, and to an even node count (pair layout)
+    while (groups.size() % (2 * kNodeGroups)) groups.push_back(Group{-1, -1, -1, -1});
 
     const size_t ng = groups.size();
     out.ngroups = static_cast<int32_t>(ng);
     out.geom.assign(ng * 16, 0.0f);
-    out.bound.assign(ng / 2 * 16, 0.0f);
+    out.bound.assign(ng / 2 * 12, 0.0f);
+    out.node.assign(ng / kNodeGroups / 2 * 12, 0.0f);
     out.index.assign(ng * 4, -1);
+    std::vector<Bound> gb(ng), nb(ng / kNodeGroups);
     for (size_t gi = 0; gi < ng; gi++) {
         const Group& g = groups[gi];
         // members: pair-SoA exactly as the linear table (r^2 = radius * radius in fp32)
@@ -100,50 +170,20 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
             base[6 + e] = r2;
             out.index[gi * 4 + k] = g[k];
         }
-        // bound: centre of the members' box (rounded to fp32 first), radius covering every
-        // member from that fp32 centre, margin coefficient Kc = 2*8*17u / r_min (tracer.hip)
-        float C[3] = {0.f, 0.f, 0.f}, R = 0.f, Rsq = 0.f, Kc = 0.f;
-        if (g[0] >= 0) {
-            double lo[3], hi[3];
-            for (int a = 0; a < 3; a++) {
-                lo[a] = std::numeric_limits<double>::infinity();
-                hi[a] = -lo[a];
-            }
-            double rmin = std::numeric_limits<double>::infinity();
-            for (int k = 0; k < 4 && g[k] >= 0; k++) {
-                const vcrt_sphere& sp = s[g[k]];
-                const double r = std::fabs(static_cast<double>(sp.radius));
-                rmin = std::min(rmin, r);
-                for (int a = 0; a < 3; a++) {
-                    lo[a] = std::min(lo[a], sp.center[a] - r);
-                    hi[a] = std::max(hi[a], sp.center[a] + r);
-                }
-            }
-            for (int a = 0; a < 3; a++) C[a] = static_cast<float>(0.5 * (lo[a] + hi[a]));
-            double rad = 0.0;
-            for (int k = 0; k < 4 && g[k] >= 0; k++) {
-                const vcrt_sphere& sp = s[g[k]];
-                double d2 = 0.0;
-                for (int a = 0; a < 3; a++) {
-                    const double d = static_cast<double>(sp.center[a]) - C[a];
-                    d2 += d * d;
-                }
-                rad = std::max(rad, std::sqrt(d2) + std::fabs(static_cast<double>(sp.radius)));
-            }
-            rad *= 1.0 + 1e-6;
-            R = round_up(rad);
-            Rsq = round_up(static_cast<double>(R) * R);
-            Kc = rmin >= 1e-3 ? round_up(1.62e-5 / rmin) : std::numeric_limits<float>::infinity();
-        }
-        float* b = &out.bound[(gi / 2) * 16];
-        const int e = gi % 2;
-        b[0 + e] = C[0];
-        b[2 + e] = C[1];
-        b[4 + e] = C[2];
-        b[6 + e] = R;
-        b[8 + e] = Rsq;
-        b[10 + e] = Kc;
+        std::vector<int32_t> members;
+        for (int k = 0; k < 4; k++)
+            if (g[k] >= 0) members.push_back(g[k]);
+        gb[gi] = bound_of(s, members);
     }
+    for (size_t ni = 0; ni < nb.size(); ni++) {
+        std::vector<int32_t> members;
+        for (size_t gi = ni * kNodeGroups; gi < (ni + 1) * kNodeGroups; gi++)
+            for (int k = 0; k < 4; k++)
+                if (groups[gi][k] >= 0) members.push_back(groups[gi][k]);
+        nb[ni] = bound_of(s, members);
+    }
+    for (size_t gi = 0; gi < ng; gi++) put_bound(out.bound, gi, gb[gi]);
+    for (size_t ni = 0; ni < nb.size(); ni++) put_bound(out.node, ni, nb[ni]);
     return true;
 }
 

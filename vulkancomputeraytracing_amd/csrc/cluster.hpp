@@ -13,10 +13,13 @@
 
 namespace vcrt {
 
+constexpr int kNodeGroups = 8;  // groups per node of the bound hierarchy
+
 struct CullTables {
-    int32_t ngroups = 0;          // even (a dummy group pads an odd count)
+    int32_t ngroups = 0;          // a multiple of 2 * kNodeGroups (padded with empty groups)
     std::vector<float> geom;      // [ngroups][16] pair-SoA, same values as the linear table
-    std::vector<float> bound;     // [ngroups / 2][16] group-pair bounds (see TraceParams.cbound)
+    std::vector<float> bound;     // [ngroups / 2][12] group-pair bounds (TraceParams.cbound)
+    std::vector<float> node;      // [ngroups / kNodeGroups / 2][12] node-pair bounds, same form
     std::vector<int32_t> index;   // [ngroups][4] world[] index of each member, -1 = padding
 };
 

@@ -167,17 +167,23 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
 }
 
 // ---------------------------------------------------------------------------------------------
-// Culled scan (variant CULL). Exact under two facts, both for finite rays (finite_ok, ray_ok):
+// Culled scan (variant CULL). Exact for waves whose rays are all in the guarded finite range
+// (|o| <= 2^30, a in [2^-20, 2^60], scene bounded), by two facts:
 //  (1) hit_sphere's sequential scan with strict < (functions.glsl:27-29,77-81) selects the
 //      candidate with the smallest t, earliest index on ties, where t = root1 if root1 > min_t
-//      else root2, kept if min_t < t < 1e5 -- so spheres may be visited in any order;
-//  (2) a group whose bounding sphere (C, R) no ray line of the wave comes within R + M of
-//      contains no sphere whose exact fp32 discriminant is >= 0. With u = 2^-24 the computed
-//      discriminant differs from a*(r^2 - dist^2) by at most ~17u*a*(|oc|^2 + r^2) (rounded oc,
-//      hb, a, cc, products, differences), so dist > r + g*|oc|^2/r with g = 17u implies disc < 0;
-//      M = Kc*(|oC|^2 + R^2) with Kc = 2*8*17u / r_min keeps an 8x safety factor (|oc| <= |oC| +
-//      R, (x+y)^2 <= 2x^2 + 2y^2), and the fp32 evaluation of the group test itself carries a
-//      1e-5 relative slack that covers its own rounding.
+//      else root2, kept if min_t < t < max_t -- so spheres may be visited in any order;
+//  (2) a margin. With u = 2^-24, disc_f >= 0 (pair_disc's rounded oc, hb, cc, products and
+//      difference) implies that the ray line passes within r + M_s of the centre,
+//      M_s = 8.1u (|oc|^2 + r^2) / r: the roundings move hb^2 - a*cc by at most ~15u a |oc|^2
+//      and the rounded oc moves the centre by u |oc|. For a bound (C, R) of members with
+//      radius >= r_min, |oc|^2 + r^2 <= 2 |oC|^2 + 3 R^2, so M = Kc (|oC|^2 + 1.5 R^2) with
+//      Kc = 32.4u / r_min covers every member twice over.
+// Bound test, per lane: with the approximate unit direction w = d * rsq(a) (|w| = 1 + O(10u))
+// and h = (o - C).w, X = |oC|^2 - h^2 approximates the squared line distance within 35u |oC|^2
+// (rounded oc, w, h, |oC|^2, X). The lane rules the bound out when X > RM^2 with
+//   RM = K |oC|^2 + Rk,  K = Kc (1 + 1e-5) + 6e-6 / (2R),  Rk = (R + 1.5 Kc R^2)(1 + 1e-5)
+// (host constants, rounded up), since RM^2 >= (R + M)^2 (1 + 2e-5) + 6e-6 |oC|^2 and 6e-6 > 35u:
+// the line then misses every member by more than its margin, so no member has disc_f >= 0.
 // Waves holding a ray outside the guarded range scan the original table in reference order.
 
 // t of one candidate as hit_sphere would accept it (finite case, fact (1)).
@@ -195,57 +201,133 @@ __device__ __forceinline__ void consider(float t, int idx, float& max_t, int& be
     }
 }
 
-__device__ __forceinline__ v2f vfma(v2f x, v2f y, v2f z) { return __builtin_elementwise_fma(x, y, z); }
+__device__ __forceinline__ v2f vfma(v2f x, v2f y, v2f z) {
+    return __builtin_elementwise_fma(x, y, z);
+}
 
+// 1 when the wave-uniform x != 0, in SALU (the compiler lowers `x ? 1 : 0` of a ballot
+// result through a VGPR: v_cndmask + v_readfirstlane per test).
+__device__ __forceinline__ uint32_t nonzero(uint64_t x) {
+    uint32_t r;
+    asm volatile("s_cmp_lg_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(r) : "s"(x) : "scc");
+    return r;
+}
+
+struct CullRay {  // one ray, splatted for packed tests
+    v2f ox, oy, oz;  // origin
+    v2f wx, wy, wz;  // approximate unit direction
+};
+
+// Bound test of one pair (TraceParams.cbound: (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1)
+// (Rk0,Rk1,-,-)): bit 0/1 set when some lane may accept a member of bound 0/1 (NaN compares as
+// "may").
+struct BoundPair {
+    float4 b0, b1;
+    float2 b2;
+};
+
+__device__ __forceinline__ BoundPair load_bound_pair(cfloat4* b) {
+    return BoundPair{b[0], b[1], *(__attribute__((address_space(4))) const float2*)(b + 2)};
+}
+
+template <bool kStats>
+__device__ __forceinline__ uint32_t bound_pair_need(const CullRay& r, const BoundPair& bp,
+                                                    uint32_t& lane_needs) {
+    const float4 b0 = bp.b0, b1 = bp.b1;
+    const float2 b2 = bp.b2;
+    const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y};
+    const v2f K = {b1.z, b1.w}, Rk = {b2.x, b2.y};
+    const v2f ocx = r.ox - Cx, ocy = r.oy - Cy, ocz = r.oz - Cz;
+    const v2f oc2 = vfma(ocz, ocz, vfma(ocy, ocy, ocx * ocx));
+    const v2f h = vfma(ocz, r.wz, vfma(ocy, r.wy, ocx * r.wx));
+    const v2f X = vfma(-h, h, oc2);   // ~ squared line distance
+    const v2f RM = vfma(K, oc2, Rk);  // >= R + M, with the slack folded in
+    const v2f T = RM * RM;
+    const uint64_t n0 = __ballot(!(X.x > T.x)), n1 = __ballot(!(X.y > T.y));
+    if constexpr (kStats) lane_needs += __popcll(n0) + __popcll(n1);
+    return nonzero(n0) | (nonzero(n1) << 1);
+}
+
+// Stats builds count in `hit_groups` the lanes that need each group (sum over group bounds).
+template <bool kStats>
 __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, const f3 d,
                                             float& max_t, int& best, uint64_t& groups_tested,
-                                            uint64_t& bounds_tested) {
+                                            uint64_t& bounds_tested, uint32_t& hit_groups) {
+    uint32_t node_lanes = 0;
     const float a = dot(d, d);
-    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const float inv = __builtin_amdgcn_rsqf(a);
+    CullRay r;
+    r.ox = (v2f){o.x, o.x};
+    r.oy = (v2f){o.y, o.y};
+    r.oz = (v2f){o.z, o.z};
+    r.wx = (v2f){d.x * inv, d.x * inv};
+    r.wy = (v2f){d.y * inv, d.y * inv};
+    r.wz = (v2f){d.z * inv, d.z * inv};
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
-    const v2f a2s = a2 * (v2f){1.0f + 1e-5f, 1.0f + 1e-5f};  // group-test slack
-    const v2f a2e = a2 * (v2f){1e-5f, 1e-5f};
     cfloat4* bound = (cfloat4*)p.cbound;
+    cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* geom = (cfloat4*)p.cgeom;
-    const int ncg = p.ncgroups;
+    const int ncg = p.ncgroups;  // multiple of 16: whole node pairs
     for (int base = 0; base < ncg; base += 64) {
-        // phase 1: which of the next 64 groups can any lane of the wave hit?
-        uint64_t need = 0;
-        const int cnt = min(64, ncg - base);
-        for (int k = 0; k < cnt; k += 2) {
-            const int bp = (base + k) >> 1;
-            const float4 b0 = bound[4 * bp], b1 = bound[4 * bp + 1], b2 = bound[4 * bp + 2];
-            const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y}, R = {b1.z, b1.w};
-            const v2f Rsq = {b2.x, b2.y}, Kc = {b2.z, b2.w};
-            const v2f ocx = ox - Cx, ocy = oy - Cy, ocz = oz - Cz;
-            const v2f oc2 = vfma(ocz, ocz, vfma(ocy, ocy, ocx * ocx));
-            const v2f hbc = vfma(ocz, dz, vfma(ocy, dy, ocx * dx));
-            const v2f X = vfma(-hbc, hbc, a2 * oc2);           // ~ a * dist^2
-            const v2f RM = vfma(Kc, oc2 + Rsq, R);             // R + M
-            const v2f thr = vfma(a2e, oc2, a2s * (RM * RM));   // ~ a * (R + M)^2 + slack
-            if (__ballot(!(X.x > thr.x))) need |= 1ull << k;
-            if (__ballot(!(X.y > thr.y))) need |= 2ull << k;
+        // level 1: which of the next (up to) 8 nodes of 8 groups may any lane hit? (the
+        // scalar loads run one pair ahead of the tests)
+        const int nn = min(8, (ncg - base) >> 3);
+        cfloat4* nb = node + 3 * (base >> 4);
+        uint32_t nodes = 0;
+        BoundPair cur = load_bound_pair(nb);
+        for (int j = 0; j < nn; j += 2) {
+            const BoundPair nxt = load_bound_pair(nb + 3 * ((j + 2 < nn ? j + 2 : j) >> 1));
+            nodes |= bound_pair_need<false>(r, cur, node_lanes) << j;
+            cur = nxt;
         }
-        bounds_tested += (uint64_t)cnt;
-        // phase 2: the exact hit_sphere test on the groups that survived
-        while (need) {
-            const int k = __builtin_ctzll(need);
+        bounds_tested += (uint64_t)(nn + 8 * __popc(nodes));
+        // level 2: which groups of those nodes?
+        uint64_t need = 0;
+        if (nodes) cur = load_bound_pair(bound + 3 * ((base + 8 * __builtin_ctz(nodes)) >> 1));
+        while (nodes) {
+            const int j = __builtin_ctz(nodes);
+            nodes &= nodes - 1;
+            cfloat4* gb = bound + 3 * ((base + 8 * j) >> 1);
+            cfloat4* gnext = bound + 3 * ((base + 8 * (nodes ? __builtin_ctz(nodes) : j)) >> 1);
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const BoundPair nxt = load_bound_pair(k + 2 < 8 ? gb + 3 * ((k + 2) >> 1) : gnext);
+                need |= (uint64_t)bound_pair_need<kStats>(r, cur, hit_groups) << (8 * j + k);
+                cur = nxt;
+            }
+        }
+        // the exact hit_sphere test on the groups that survived (next group prefetched)
+        groups_tested += (uint64_t)__popcll(need);
+        if (!need) continue;
+        int gi = base + __builtin_ctzll(need);
+        float4 q0 = geom[4 * gi], q1 = geom[4 * gi + 1], q2 = geom[4 * gi + 2],
+               q3 = geom[4 * gi + 3];
+        while (true) {
             need &= need - 1;
-            const int gi = base + k;
-            ++groups_tested;
-            const float4 q0 = geom[4 * gi], q1 = geom[4 * gi + 1], q2 = geom[4 * gi + 2],
-                         q3 = geom[4 * gi + 3];
+            const int gn = need ? base + __builtin_ctzll(need) : gi;
+            const float4 n0 = geom[4 * gn], n1 = geom[4 * gn + 1], n2 = geom[4 * gn + 2],
+                         n3 = geom[4 * gn + 3];
             v2f hb01, d01, hb23, d23;
-            pair_disc(ox, oy, oz, dx, dy, dz, a2, q0, q1, hb01, d01);
-            pair_disc(ox, oy, oz, dx, dy, dz, a2, q2, q3, hb23, d23);
+            pair_disc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, d01);
+            pair_disc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, d23);
             const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
             if (__ballot(!(m4 < 0.0f))) {
                 const int4 id = ((__attribute__((address_space(4))) const int4*)p.cindex)[gi];
-                if (!(d01.x < 0.0f) && id.x >= 0) consider(candidate_t(hb01.x, d01.x, a), id.x, max_t, best);
-                if (!(d01.y < 0.0f) && id.y >= 0) consider(candidate_t(hb01.y, d01.y, a), id.y, max_t, best);
-                if (!(d23.x < 0.0f) && id.z >= 0) consider(candidate_t(hb23.x, d23.x, a), id.z, max_t, best);
-                if (!(d23.y < 0.0f) && id.w >= 0) consider(candidate_t(hb23.y, d23.y, a), id.w, max_t, best);
+                if (!(d01.x < 0.0f) && id.x >= 0)
+                    consider(candidate_t(hb01.x, d01.x, a), id.x, max_t, best);
+                if (!(d01.y < 0.0f) && id.y >= 0)
+                    consider(candidate_t(hb01.y, d01.y, a), id.y, max_t, best);
+                if (!(d23.x < 0.0f) && id.z >= 0)
+                    consider(candidate_t(hb23.x, d23.x, a), id.z, max_t, best);
+                if (!(d23.y < 0.0f) && id.w >= 0)
+                    consider(candidate_t(hb23.y, d23.y, a), id.w, max_t, best);
             }
+            if (!need) break;
+            gi = gn;
+            q0 = n0;
+            q1 = n1;
+            q2 = n2;
+            q3 = n3;
         }
     }
 }
@@ -356,7 +438,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                                  aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(!guarded) == 0) {
-                scan_culled(p, o, d, max_t, best, w_groups, w_bounds);
+                scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups);
             } else {
                 scan_spheres<false>(p, lds_geom, n, o, d, max_t, best, hit_groups);
                 w_groups += (uint64_t)((n + 3) >> 2);
