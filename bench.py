@@ -20,6 +20,9 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector, MI355X_MICROARCH.md chip table
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
+FLOPS_PER_BOUND_TEST = 18       # tracer.hip bound_pair_need, per bound: oc 3, |oC|^2 5, h 5,
+                                # X 2, RM 2, RM^2 1
+KERNEL_NAMES = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull"}
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -182,6 +185,13 @@ def main():
         seg = sum(segments) / len(segments)
         flops = seg * nspheres * FLOPS_PER_SPHERE_TEST
         achieved = flops / (k_ms * 1e-3) / 1e12
+        # The culled scan skips most of the reference's per-segment sphere tests (same bits),
+        # so the algorithmic rate above counts work it never issued; the flops it did issue
+        # (every lane of each wave-level group test and bound test) bound the VALU side.
+        executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
+                    + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
+        if st["kernel_variant"] != 3:
+            executed = flops
         traffic = None
         if os.path.exists(PROFILE_TRAFFIC):
             try:
@@ -215,10 +225,14 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                         "kernel": "vcrt_trace_lds" if st["kernel_variant"] == 1
-                         else "vcrt_trace_smem",
+                         "kernel": KERNEL_NAMES.get(st["kernel_variant"], "?"),
                          "kernel_ms": round(k_ms, 3), "segments_per_launch": int(seg),
-                         "flops_per_launch": flops},
+                         "flops_per_launch": flops,
+                         "numerator": "algorithmic: segments x spheres x 23 (SURVEY 8(d))",
+                         "executed_flops_per_launch": executed,
+                         "executed_tflops": round(executed / (k_ms * 1e-3) / 1e12, 3),
+                         "executed_frac": round(executed / (k_ms * 1e-3) / 1e12
+                                                / PEAK_FP32_TFLOPS, 4)},
         }
         if validated is not None:
             out["validated_bitwise_vs_1gpu"] = validated

@@ -71,7 +71,8 @@ typedef struct vcrt_camera { /* globals.glsl:21-24 */
 /* Kernel variants. SMEM: wave-uniform scalar-cache reads of the linear sphere table (measured
  * faster than LDS staging for 485 and 4100 spheres). CULL: spheres grouped
  * spatially in fours, a group is tested only when some ray of the wave may come near it (same
- * results bit for bit; falls back to SMEM below 16 spheres or for unbounded scenes). */
+ * results bit for bit; falls back to SMEM below 16 spheres or for unbounded scenes). AUTO =
+ * CULL when it applies, else SMEM. */
 #define VCRT_KERNEL_AUTO 0
 #define VCRT_KERNEL_LDS 1
 #define VCRT_KERNEL_SMEM 2

@@ -38,14 +38,15 @@ for name in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
 with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
     json.dump(summary, f, indent=1)
 
-fetch = summary["pmc_fetch"]["vcrt_trace_smem|FETCH_SIZE"]
-write = summary["pmc_write"]["vcrt_trace_smem|WRITE_SIZE"]
+kernel = bench["roofline"]["kernel"]
+fetch = summary["pmc_fetch"][f"{kernel}|FETCH_SIZE"]
+write = summary["pmc_write"][f"{kernel}|WRITE_SIZE"]
 per_launch = (2 * fetch["sum"] / fetch["dispatches"] + write["sum"] / write["dispatches"]) * 1024
 cfg = bench["config"]
 key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_s{cfg['spp']}_d{cfg['max_depth']}_n1"
 traffic_path = os.path.join(dst, "traffic.json")
 traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
-traffic[key] = {"hbm_bytes_per_launch": per_launch, "fetch_kb": fetch["sum"] / fetch["dispatches"],
+traffic[key] = {"hbm_bytes_per_launch": per_launch, "kernel": kernel, "fetch_kb": fetch["sum"] / fetch["dispatches"],
                 "write_kb": write["sum"] / write["dispatches"], "round": tag,
                 "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/render_once.py "
                         "at the bench config; FETCH_SIZE doubled (gfx950 correction)"}

@@ -508,11 +508,12 @@ vcrt_result vcrt_draw_next_frame(void) {
         // scan table: (groups + 1 padding group) x 64 B
         const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
         int variant = g.desc.kernel_variant;
-        // Measured on MI355X: the scalar-cache variant keeps the sphere data in SGPRs (no
-        // VGPRs, no LDS traffic, 7 waves/SIMD vs 5) and beats LDS staging by 15% on the
-        // 485-sphere scene and by 18% on the 4100-sphere stress scene (65 KB table, served
-        // from L2 behind the one-group prefetch), so AUTO always picks it.
-        if (variant == VCRT_KERNEL_AUTO) variant = VCRT_KERNEL_SMEM;
+        // Measured on MI355X: of the linear scans the scalar-cache variant (sphere data in
+        // SGPRs, no LDS traffic) beats LDS staging by 15% (485 spheres) and 18% (4100); the
+        // culled scan beats both (+29% / +75%, same bits), so AUTO picks CULL whenever the
+        // scene has its tables (>= 16 spheres, bounded) and SMEM otherwise.
+        if (variant == VCRT_KERNEL_AUTO)
+            variant = g.ncgroups > 0 ? VCRT_KERNEL_CULL : VCRT_KERNEL_SMEM;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
         if (variant == VCRT_KERNEL_CULL && g.ncgroups == 0) variant = VCRT_KERNEL_SMEM;
         hipFunction_t f = variant == VCRT_KERNEL_LDS    ? g.k_trace_lds

@@ -232,7 +232,7 @@ __device__ __forceinline__ BoundPair load_bound_pair(cfloat4* b) {
 
 template <bool kStats>
 __device__ __forceinline__ uint32_t bound_pair_need(const CullRay& r, const BoundPair& bp,
-                                                    uint32_t& lane_needs) {
+                                                    uint32_t& lane_needs, uint32_t& lane_cnt) {
     const float4 b0 = bp.b0, b1 = bp.b1;
     const float2 b2 = bp.b2;
     const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y};
@@ -244,16 +244,21 @@ __device__ __forceinline__ uint32_t bound_pair_need(const CullRay& r, const Boun
     const v2f RM = vfma(K, oc2, Rk);  // >= R + M, with the slack folded in
     const v2f T = RM * RM;
     const uint64_t n0 = __ballot(!(X.x > T.x)), n1 = __ballot(!(X.y > T.y));
-    if constexpr (kStats) lane_needs += __popcll(n0) + __popcll(n1);
+    if constexpr (kStats) {
+        lane_needs += __popcll(n0) + __popcll(n1);
+        lane_cnt += (uint32_t)!(X.x > T.x) + (uint32_t)!(X.y > T.y);
+    }
     return nonzero(n0) | (nonzero(n1) << 1);
 }
 
-// Stats builds count in `hit_groups` the lanes that need each group (sum over group bounds).
+// Stats builds count in `hit_groups` the lanes that need each group (sum over group bounds)
+// and in `lane_cnt` the groups this lane needs.
 template <bool kStats>
 __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, const f3 d,
                                             float& max_t, int& best, uint64_t& groups_tested,
-                                            uint64_t& bounds_tested, uint32_t& hit_groups) {
-    uint32_t node_lanes = 0;
+                                            uint64_t& bounds_tested, uint32_t& hit_groups,
+                                            uint32_t& lane_cnt) {
+    uint32_t node_lanes = 0, node_cnt = 0;
     const float a = dot(d, d);
     const float inv = __builtin_amdgcn_rsqf(a);
     CullRay r;
@@ -277,7 +282,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
         BoundPair cur = load_bound_pair(nb);
         for (int j = 0; j < nn; j += 2) {
             const BoundPair nxt = load_bound_pair(nb + 3 * ((j + 2 < nn ? j + 2 : j) >> 1));
-            nodes |= bound_pair_need<false>(r, cur, node_lanes) << j;
+            nodes |= bound_pair_need<false>(r, cur, node_lanes, node_cnt) << j;
             cur = nxt;
         }
         bounds_tested += (uint64_t)(nn + 8 * __popc(nodes));
@@ -292,7 +297,8 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
 #pragma unroll
             for (int k = 0; k < 8; k += 2) {
                 const BoundPair nxt = load_bound_pair(k + 2 < 8 ? gb + 3 * ((k + 2) >> 1) : gnext);
-                need |= (uint64_t)bound_pair_need<kStats>(r, cur, hit_groups) << (8 * j + k);
+                need |= (uint64_t)bound_pair_need<kStats>(r, cur, hit_groups, lane_cnt)
+                        << (8 * j + k);
                 cur = nxt;
             }
         }
@@ -380,7 +386,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         // ---- lanes whose item is finished take the next ones (one atomic per wave) ----
         uint64_t need_mask = __ballot(need && !done);
         while (need_mask) {
-            if constexpr (kStats) ++st_fetch;
+            if constexpr (kStats && !kCull) ++st_fetch;
             const int leader = __ffsll((unsigned long long)need_mask) - 1;
             uint32_t base = 0;
             if ((int)lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need_mask));
@@ -438,7 +444,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                                  aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(!guarded) == 0) {
-                scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups);
+                uint32_t lane_cnt = 0;
+                scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
+                                    lane_cnt);
+                if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
+                    for (int off = 32; off > 0; off >>= 1)
+                        lane_cnt = max(lane_cnt, (uint32_t)__shfl_xor((int)lane_cnt, off));
+                    st_fetch += lane_cnt;
+                }
             } else {
                 scan_spheres<false>(p, lds_geom, n, o, d, max_t, best, hit_groups);
                 w_groups += (uint64_t)((n + 3) >> 2);
