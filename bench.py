@@ -22,7 +22,8 @@ PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector, MI355X_MICROARCH.md chip t
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
 FLOPS_PER_BOUND_TEST = 18       # tracer.hip bound_pair_need, per bound: oc 3, |oC|^2 5, h 5,
                                 # X 2, RM 2, RM^2 1
-KERNEL_NAMES = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull"}
+KERNEL_NAMES = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull",
+                4: "vcrt_trace_cull_lane"}
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -190,8 +191,11 @@ def main():
         # (every lane of each wave-level group test and bound test) bound the VALU side.
         executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
                     + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
-        if st["kernel_variant"] != 3:
+        if st["kernel_variant"] not in (3, 4):
             executed = flops
+        kernel = KERNEL_NAMES.get(st["kernel_variant"], "?")
+        if st["kernel_variant"] == 4 and st["lds_bytes"] > 0:
+            kernel += "_lds"
         traffic = None
         if os.path.exists(PROFILE_TRAFFIC):
             try:
@@ -225,7 +229,7 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                         "kernel": KERNEL_NAMES.get(st["kernel_variant"], "?"),
+                         "kernel": kernel,
                          "kernel_ms": round(k_ms, 3), "segments_per_launch": int(seg),
                          "flops_per_launch": flops,
                          "numerator": "algorithmic: segments x spheres x 23 (SURVEY 8(d))",

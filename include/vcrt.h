@@ -77,6 +77,7 @@ typedef struct vcrt_camera { /* globals.glsl:21-24 */
 #define VCRT_KERNEL_LDS 1
 #define VCRT_KERNEL_SMEM 2
 #define VCRT_KERNEL_CULL 3
+#define VCRT_KERNEL_CULL_LANE 4 /* CULL with per-lane group tests (LDS or global tables) */
 
 typedef struct vcrt_render_desc {
     uint32_t struct_size;      /* sizeof(vcrt_render_desc) */

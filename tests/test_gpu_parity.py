@@ -54,12 +54,13 @@ CASES = [
 ]
 
 
-VARIANTS = [vc.KERNEL_LDS, vc.KERNEL_SMEM, vc.KERNEL_CULL]
+VARIANTS = [vc.KERNEL_LDS, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE]
+CULLED = (vc.KERNEL_CULL, vc.KERNEL_CULL_LANE)
 
 
 def expected_variant(variant, nspheres):
-    # CULL needs >= 16 spheres (vcrt.h); below that the linear SMEM scan runs
-    return vc.KERNEL_SMEM if variant == vc.KERNEL_CULL and nspheres < 16 else variant
+    # the culled scans need >= 16 spheres (vcrt.h); below that the linear SMEM scan runs
+    return vc.KERNEL_SMEM if variant in CULLED and nspheres < 16 else variant
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -111,10 +112,26 @@ def test_golden_oracle_images():
 def test_stress_scene_small(oracle):
     w, h, spp, depth = 48, 27, 2, 10
     want, segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("stress4096"))
-    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL):
+    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE):
         got, st = gpu_render("stress4096", w, h, spp, depth, variant)
         assert_bitwise(got, want, f"stress v{variant}")
         assert st["segments"] == segs and st["nspheres"] == 4100
+
+
+@pytest.mark.parametrize("tables", ["lds", "global"])
+@pytest.mark.parametrize("scene", ["final", "stress4096"])
+def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene):
+    # the per-lane scan gathers table rows from an LDS copy or from global memory
+    # (VCRT_CULL_LANE_TABLES forces either; the default picks LDS up to 32 KB)
+    monkeypatch.setenv("VCRT_CULL_LANE_TABLES", tables)
+    w, h, spp, depth = 40, 24, 3, 12
+    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
+    got, st = gpu_render(scene, w, h, spp, depth, vc.KERNEL_CULL_LANE)
+    assert st["kernel_variant"] == vc.KERNEL_CULL_LANE
+    assert_bitwise(got, want, f"{scene} lane tables={tables}")
+    assert st["segments"] == segs
+    assert (st["lds_bytes"] > 0) == (tables == "lds")
 
 
 def culling_torture_scene():
@@ -146,7 +163,7 @@ def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
     cfg = dict(lookfrom=(6, 2.5, 5), lookat=(0, 0.6, 0), vfov=45)
     k = vc.renderer.effective_chunk(spp, chunk, pixels=vc.tile_slots(w, h))
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
-    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL):
+    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, kernel_variant=variant, accumulate_chunk=chunk, **cfg)
         with vc.Renderer(desc, sc) as r:
@@ -155,7 +172,7 @@ def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
         assert st["kernel_variant"] == variant
         assert_bitwise(got, want, f"torture v{variant}")
         assert st["segments"] == segs
-        if variant == vc.KERNEL_CULL:
+        if variant in CULLED:
             assert 0 < st["group_tests"]
             assert st["bound_tests"] > 0
 
@@ -278,7 +295,7 @@ def test_reference_named_lifecycle():
     vc.SetRenderScene(None)
 
 
-@pytest.mark.parametrize("variant", [vc.KERNEL_AUTO, vc.KERNEL_CULL])
+@pytest.mark.parametrize("variant", [vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL_LANE])
 def test_full_size_rows_subset_rms(oracle, variant):
     # BASELINE config 3 geometry (1920x1080, depth 10) at 16 spp; oracle renders every 90th row.
     w, h, spp, depth = 1920, 1080, 16, 10

@@ -33,6 +33,7 @@ KERNEL_AUTO = 0
 KERNEL_LDS = 1
 KERNEL_SMEM = 2
 KERNEL_CULL = 3
+KERNEL_CULL_LANE = 4
 
 SCENE_FINAL = 0
 SCENE_THREE = 1

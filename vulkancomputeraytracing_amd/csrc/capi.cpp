@@ -46,7 +46,10 @@ struct RendererState {
     hipFunction_t k_trace_lds = nullptr, k_trace_smem = nullptr, k_assemble = nullptr,
                   k_fill = nullptr, k_trace_lds_stats = nullptr, k_trace_smem_stats = nullptr,
                   k_resolve = nullptr, k_encode = nullptr, k_trace_cull = nullptr,
-                  k_trace_cull_stats = nullptr;
+                  k_trace_cull_stats = nullptr, k_trace_cull_lane_lds = nullptr,
+                  k_trace_cull_lane_lds_stats = nullptr, k_trace_cull_lane = nullptr,
+                  k_trace_cull_lane_stats = nullptr;
+    int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
     bool debug_stats = false;
     uint32_t work_flags = 0;
@@ -60,10 +63,9 @@ struct RendererState {
     float* d_material = nullptr;
     // culled-scan tables (cluster.hpp); ncgroups == 0 when culling does not apply
     int32_t ncgroups = 0;
-    float4* d_cgeom = nullptr;
+    float4* d_cgroup = nullptr;
     float4* d_cbound = nullptr;
     float4* d_cnode = nullptr;
-    int4* d_cindex = nullptr;
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
     uint32_t total_pixels = 0, total_items = 0;
@@ -155,14 +157,12 @@ void free_scene() {
     g.d_center_radius = nullptr;
     g.d_shade = nullptr;
     g.d_material = nullptr;
-    if (g.d_cgeom) (void)hipFree(g.d_cgeom);
+    if (g.d_cgroup) (void)hipFree(g.d_cgroup);
     if (g.d_cbound) (void)hipFree(g.d_cbound);
     if (g.d_cnode) (void)hipFree(g.d_cnode);
-    if (g.d_cindex) (void)hipFree(g.d_cindex);
-    g.d_cgeom = nullptr;
+    g.d_cgroup = nullptr;
     g.d_cbound = nullptr;
     g.d_cnode = nullptr;
-    g.d_cindex = nullptr;
     g.ncgroups = 0;
     g.nspheres = 0;
 }
@@ -179,6 +179,11 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull, m, "vcrt_trace_cull"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_stats, m, "vcrt_trace_cull_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds, m, "vcrt_trace_cull_lane_lds"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_stats, m,
+                                  "vcrt_trace_cull_lane_lds_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane, m, "vcrt_trace_cull_lane"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_stats, m, "vcrt_trace_cull_lane_stats"));
     return VK_SUCCESS;
 }
 
@@ -209,7 +214,7 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
     if (d.progressive != 0 && d.progressive != 1) return false;
-    if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL) return false;
+    if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL_LANE) return false;
     return true;
 }
 
@@ -349,6 +354,8 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
     if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VCRT_CULL_LANE_TABLES"))
+        g.cull_lane_tables = std::strcmp(e, "lds") == 0 ? 1 : std::strcmp(e, "global") == 0 ? 2 : 0;
     if (const char* e = std::getenv("VCRT_WORK_ORDER"))
         if (std::strcmp(e, "reverse") == 0) g.work_flags |= vcrt::kFlagReverseOrder;
     if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, 64))) != VK_SUCCESS) return fail(r);
@@ -403,17 +410,20 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     (void)hipStreamSynchronize(g.stream);
     free_scene();
     if (ct.ngroups > 0) {
-        VCRT_TRY(hipMalloc(&g.d_cgeom, sizeof(float) * ct.geom.size()));
+        // group records: the four pair-SoA float4s + the member indices (int bits)
+        std::vector<float> rec(static_cast<size_t>(ct.ngroups) * 20);
+        for (int32_t gi = 0; gi < ct.ngroups; gi++) {
+            std::memcpy(&rec[gi * 20], &ct.geom[gi * 16], 16 * sizeof(float));
+            std::memcpy(&rec[gi * 20 + 16], &ct.index[gi * 4], 4 * sizeof(int32_t));
+        }
+        VCRT_TRY(hipMalloc(&g.d_cgroup, sizeof(float) * rec.size()));
         VCRT_TRY(hipMalloc(&g.d_cbound, sizeof(float) * ct.bound.size()));
         VCRT_TRY(hipMalloc(&g.d_cnode, sizeof(float) * ct.node.size()));
-        VCRT_TRY(hipMalloc(&g.d_cindex, sizeof(int32_t) * ct.index.size()));
-        VCRT_TRY(hipMemcpy(g.d_cnode, ct.node.data(), sizeof(float) * ct.node.size(),
-                           hipMemcpyHostToDevice));
-        VCRT_TRY(hipMemcpy(g.d_cgeom, ct.geom.data(), sizeof(float) * ct.geom.size(),
+        VCRT_TRY(hipMemcpy(g.d_cgroup, rec.data(), sizeof(float) * rec.size(),
                            hipMemcpyHostToDevice));
         VCRT_TRY(hipMemcpy(g.d_cbound, ct.bound.data(), sizeof(float) * ct.bound.size(),
                            hipMemcpyHostToDevice));
-        VCRT_TRY(hipMemcpy(g.d_cindex, ct.index.data(), sizeof(int32_t) * ct.index.size(),
+        VCRT_TRY(hipMemcpy(g.d_cnode, ct.node.data(), sizeof(float) * ct.node.size(),
                            hipMemcpyHostToDevice));
         g.ncgroups = ct.ngroups;
     }
@@ -480,10 +490,9 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
         p.debug = static_cast<unsigned long long*>(g.d_debug);
         p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);
-        p.cgeom = g.d_cgeom;
+        p.cgroup = g.d_cgroup;
         p.cbound = g.d_cbound;
         p.cnode = g.d_cnode;
-        p.cindex = g.d_cindex;
         p.ncgroups = g.ncgroups;
         p.nspheres = g.nspheres;
         p.width = g.desc.width;
@@ -507,23 +516,44 @@ vcrt_result vcrt_draw_next_frame(void) {
         }
         // scan table: (groups + 1 padding group) x 64 B
         const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
+        // per-lane culled scan: tables in LDS when they fit in 32 KB (5+ workgroups per CU)
+        const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 3 + g.ncgroups * 5));
+        const bool lane_lds = tab_lds <= g.max_lds &&
+                              (g.cull_lane_tables == 1 ||
+                               (g.cull_lane_tables == 0 && tab_lds <= 32768u));
         int variant = g.desc.kernel_variant;
         // Measured on MI355X: of the linear scans the scalar-cache variant (sphere data in
         // SGPRs, no LDS traffic) beats LDS staging by 15% (485 spheres) and 18% (4100); the
-        // culled scan beats both (+29% / +75%, same bits), so AUTO picks CULL whenever the
-        // scene has its tables (>= 16 spheres, bounded) and SMEM otherwise.
+        // culled scans beat both (same bits). AUTO: the per-lane culled scan when its tables
+        // fit in LDS (485 spheres: +46% over SMEM, +10% over CULL), else the wave-uniform
+        // culled scan (4100 spheres: +75% over SMEM; per-lane on global tables is ~5% slower),
+        // and SMEM when the scene has no tables (< 16 spheres or unbounded).
         if (variant == VCRT_KERNEL_AUTO)
-            variant = g.ncgroups > 0 ? VCRT_KERNEL_CULL : VCRT_KERNEL_SMEM;
+            variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM
+                      : lane_lds      ? VCRT_KERNEL_CULL_LANE
+                                      : VCRT_KERNEL_CULL;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
-        if (variant == VCRT_KERNEL_CULL && g.ncgroups == 0) variant = VCRT_KERNEL_SMEM;
-        hipFunction_t f = variant == VCRT_KERNEL_LDS    ? g.k_trace_lds
-                          : variant == VCRT_KERNEL_CULL ? g.k_trace_cull
-                                                        : g.k_trace_smem;
-        if (g.debug_stats)
-            f = variant == VCRT_KERNEL_LDS    ? g.k_trace_lds_stats
-                : variant == VCRT_KERNEL_CULL ? g.k_trace_cull_stats
-                                              : g.k_trace_smem_stats;
-        const uint32_t lds = variant == VCRT_KERNEL_LDS ? geom_lds : 0;
+        if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE) &&
+            g.ncgroups == 0)
+            variant = VCRT_KERNEL_SMEM;
+        hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
+        uint32_t lds = 0;
+        if (variant == VCRT_KERNEL_LDS) {
+            f = g.k_trace_lds;
+            fs = g.k_trace_lds_stats;
+            lds = geom_lds;
+        } else if (variant == VCRT_KERNEL_CULL) {
+            f = g.k_trace_cull;
+            fs = g.k_trace_cull_stats;
+        } else if (variant == VCRT_KERNEL_CULL_LANE && lane_lds) {
+            f = g.k_trace_cull_lane_lds;
+            fs = g.k_trace_cull_lane_lds_stats;
+            lds = tab_lds;
+        } else if (variant == VCRT_KERNEL_CULL_LANE) {
+            f = g.k_trace_cull_lane;
+            fs = g.k_trace_cull_lane_stats;
+        }
+        if (g.debug_stats) f = fs;
         const uint32_t block = 256;
         int per_cu = g.desc.blocks_per_cu;
         if (per_cu <= 0) {

@@ -194,6 +194,26 @@ __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
     return (-hb + sq) / a;
 }
 
+// A member whose origin lies outside or on it (cc >= 0) while the ray points away from its
+// centre (hb >= 0) can never be accepted: disc_f <= RN(hb^2), RN(sqrt(RN(hb^2))) = hb, so
+// RN(-hb + sq) <= 0 and both roots are <= 0 < min_t. (Padding members never hit: their
+// r^2 = -3e38 makes disc negative or -inf.)
+__device__ __forceinline__ bool may_hit(float hb, float cc, float disc) {
+    return !(disc < 0.0f) && (hb < 0.0f || cc < 0.0f);
+}
+
+// pair_disc that also returns cc = |oc|^2 - r^2 (for may_hit).
+__device__ __forceinline__ void pair_disc_cc(const v2f ox, const v2f oy, const v2f oz,
+                                             const v2f dx, const v2f dy, const v2f dz,
+                                             const v2f a2, float4 xy, float4 zr, v2f& hb,
+                                             v2f& cc, v2f& disc) {
+    const v2f cx = {xy.x, xy.y}, cy = {xy.z, xy.w}, cz = {zr.x, zr.y}, r2 = {zr.z, zr.w};
+    const v2f ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    hb = ocx * dx + ocy * dy + ocz * dz;
+    cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
+    disc = hb * hb - a2 * cc;
+}
+
 __device__ __forceinline__ void consider(float t, int idx, float& max_t, int& best) {
     if (t > 0.001f && (t < max_t || (t == max_t && best >= 0 && idx < best))) {
         max_t = t;
@@ -271,7 +291,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     cfloat4* bound = (cfloat4*)p.cbound;
     cfloat4* node = (cfloat4*)p.cnode;
-    cfloat4* geom = (cfloat4*)p.cgeom;
+    cfloat4* geom = (cfloat4*)p.cgroup;
     const int ncg = p.ncgroups;  // multiple of 16: whole node pairs
     for (int base = 0; base < ncg; base += 64) {
         // level 1: which of the next (up to) 8 nodes of 8 groups may any lane hit? (the
@@ -306,26 +326,28 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
         groups_tested += (uint64_t)__popcll(need);
         if (!need) continue;
         int gi = base + __builtin_ctzll(need);
-        float4 q0 = geom[4 * gi], q1 = geom[4 * gi + 1], q2 = geom[4 * gi + 2],
-               q3 = geom[4 * gi + 3];
+        float4 q0 = geom[5 * gi], q1 = geom[5 * gi + 1], q2 = geom[5 * gi + 2],
+               q3 = geom[5 * gi + 3];
         while (true) {
             need &= need - 1;
             const int gn = need ? base + __builtin_ctzll(need) : gi;
-            const float4 n0 = geom[4 * gn], n1 = geom[4 * gn + 1], n2 = geom[4 * gn + 2],
-                         n3 = geom[4 * gn + 3];
-            v2f hb01, d01, hb23, d23;
-            pair_disc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, d01);
-            pair_disc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, d23);
+            const float4 n0 = geom[5 * gn], n1 = geom[5 * gn + 1], n2 = geom[5 * gn + 2],
+                         n3 = geom[5 * gn + 3];
+            v2f hb01, cc01, d01, hb23, cc23, d23;
+            pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+            pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
             const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
             if (__ballot(!(m4 < 0.0f))) {
-                const int4 id = ((__attribute__((address_space(4))) const int4*)p.cindex)[gi];
-                if (!(d01.x < 0.0f) && id.x >= 0)
+                const float4 idf = geom[5 * gi + 4];
+                const int4 id = make_int4(__float_as_int(idf.x), __float_as_int(idf.y),
+                                          __float_as_int(idf.z), __float_as_int(idf.w));
+                if (may_hit(hb01.x, cc01.x, d01.x))
                     consider(candidate_t(hb01.x, d01.x, a), id.x, max_t, best);
-                if (!(d01.y < 0.0f) && id.y >= 0)
+                if (may_hit(hb01.y, cc01.y, d01.y))
                     consider(candidate_t(hb01.y, d01.y, a), id.y, max_t, best);
-                if (!(d23.x < 0.0f) && id.z >= 0)
+                if (may_hit(hb23.x, cc23.x, d23.x))
                     consider(candidate_t(hb23.x, d23.x, a), id.z, max_t, best);
-                if (!(d23.y < 0.0f) && id.w >= 0)
+                if (may_hit(hb23.y, cc23.y, d23.y))
                     consider(candidate_t(hb23.y, d23.y, a), id.w, max_t, best);
             }
             if (!need) break;
@@ -334,6 +356,105 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
             q1 = n1;
             q2 = n2;
             q3 = n3;
+        }
+    }
+}
+
+// Per-lane culled scan (variant CULL_LANE). Same tables and tests as scan_culled, but only
+// the node level runs wave-uniformly (scalar loads, per-lane results); each lane then tests
+// the groups of its own nodes and runs the exact test on its own groups, gathering table rows
+// with per-lane addresses (from an LDS copy, or from global memory when the tables are too
+// large). A wave's work becomes the largest per-lane need instead of the union over lanes.
+// Lanes accept candidates with the same `consider` rule, so the result is the same.
+
+// Per-lane bound test of one pair (any operands): bit 0/1 = this lane may need bound 0/1.
+__device__ __forceinline__ uint32_t bound_pair_bits(const CullRay& r, float4 b0, float4 b1,
+                                                    float2 b2) {
+    const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y};
+    const v2f K = {b1.z, b1.w}, Rk = {b2.x, b2.y};
+    const v2f ocx = r.ox - Cx, ocy = r.oy - Cy, ocz = r.oz - Cz;
+    const v2f oc2 = vfma(ocz, ocz, vfma(ocy, ocy, ocx * ocx));
+    const v2f h = vfma(ocz, r.wz, vfma(ocy, r.wy, ocx * r.wx));
+    const v2f X = vfma(-h, h, oc2);
+    const v2f RM = vfma(K, oc2, Rk);
+    const v2f T = RM * RM;
+    return (uint32_t)!(X.x > T.x) | ((uint32_t)!(X.y > T.y) << 1);
+}
+
+template <bool kStats>
+__device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const float4* tbound,
+                                                 const float4* tgroup, const f3 o, const f3 d,
+                                                 float& max_t, int& best,
+                                                 uint64_t& groups_tested,
+                                                 uint64_t& bounds_tested, uint32_t& lane_cnt) {
+    const float a = dot(d, d);
+    const float inv = __builtin_amdgcn_rsqf(a);
+    CullRay r;
+    r.ox = (v2f){o.x, o.x};
+    r.oy = (v2f){o.y, o.y};
+    r.oz = (v2f){o.z, o.z};
+    r.wx = (v2f){d.x * inv, d.x * inv};
+    r.wy = (v2f){d.y * inv, d.y * inv};
+    r.wz = (v2f){d.z * inv, d.z * inv};
+    const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
+    cfloat4* node = (cfloat4*)p.cnode;
+    const int ncg = p.ncgroups;
+    for (int base = 0; base < ncg; base += 64) {
+        // level 1, wave-uniform: nodes of this chunk, per-lane bits
+        const int nn = min(8, (ncg - base) >> 3);
+        cfloat4* nb = node + 3 * (base >> 4);
+        uint32_t nodes = 0;
+        BoundPair cur = load_bound_pair(nb);
+        for (int j = 0; j < nn; j += 2) {
+            const BoundPair nxt = load_bound_pair(nb + 3 * ((j + 2 < nn ? j + 2 : j) >> 1));
+            nodes |= bound_pair_bits(r, cur.b0, cur.b1, cur.b2) << j;
+            cur = nxt;
+        }
+        bounds_tested += (uint64_t)nn;
+        // level 2, per lane: the groups of this lane's nodes
+        uint64_t need = 0;
+        while (__ballot(nodes != 0)) {
+            bounds_tested += 8;  // one wave pass = 8 bound tests
+            if (nodes) {
+                const int j = __builtin_ctz(nodes);
+                nodes &= nodes - 1;
+                const float4* gb = tbound + 3 * ((base + 8 * j) >> 1);
+                uint32_t bits = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float4 b0 = gb[3 * k], b1 = gb[3 * k + 1], b2 = gb[3 * k + 2];
+                    bits |= bound_pair_bits(r, b0, b1, make_float2(b2.x, b2.y)) << (2 * k);
+                }
+                need |= (uint64_t)bits << (8 * j);
+            }
+        }
+        if constexpr (kStats) lane_cnt += (uint32_t)__popcll(need);
+        // the exact test, per lane on its own groups
+        while (__ballot(need != 0)) {
+            ++groups_tested;
+            if (need) {
+                const int k = __builtin_ctzll(need);
+                need &= need - 1;
+                const float4* g = tgroup + 5 * (base + k);
+                const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3], idf = g[4];
+                v2f hb01, cc01, d01, hb23, cc23, d23;
+                pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+                pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+                const int i0 = __float_as_int(idf.x), i1 = __float_as_int(idf.y),
+                          i2 = __float_as_int(idf.z), i3 = __float_as_int(idf.w);
+                uint32_t hits = (uint32_t)may_hit(hb01.x, cc01.x, d01.x) |
+                                ((uint32_t)may_hit(hb01.y, cc01.y, d01.y) << 1) |
+                                ((uint32_t)may_hit(hb23.x, cc23.x, d23.x) << 2) |
+                                ((uint32_t)may_hit(hb23.y, cc23.y, d23.y) << 3);
+                while (hits) {
+                    const int s = __builtin_ctz(hits);
+                    hits &= hits - 1;
+                    const float hb = s == 0 ? hb01.x : s == 1 ? hb01.y : s == 2 ? hb23.x : hb23.y;
+                    const float ds = s == 0 ? d01.x : s == 1 ? d01.y : s == 2 ? d23.x : d23.y;
+                    const int idx = s == 0 ? i0 : s == 1 ? i1 : s == 2 ? i2 : i3;
+                    consider(candidate_t(hb, ds, a), idx, max_t, best);
+                }
+            }
         }
     }
 }
@@ -357,13 +478,25 @@ __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, ui
     return px;
 }
 
-template <bool kLds, bool kStats, bool kCull = false>
+// kCull: 0 = linear scan (kLds: table in LDS), 1 = culled scan, 2 = per-lane culled scan
+// with the group tables copied to LDS, 3 = per-lane culled scan on global tables.
+template <bool kLds, bool kStats, int kCull = 0>
 __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geom) {
     const int n = p.nspheres;
     if constexpr (kLds) {
         const int nq = 4 * (((n + 3) >> 2) + 1);
         for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = p.geom[i];
         __syncthreads();
+    }
+    const float4* tbound = p.cbound;
+    const float4* tgroup = p.cgroup;
+    if constexpr (kCull == 2) {
+        const int nb = (p.ncgroups >> 1) * 3, ng = p.ncgroups * 5;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = p.cbound[i];
+        for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = p.cgroup[i];
+        __syncthreads();
+        tbound = lds_geom;
+        tgroup = lds_geom + nb;
     }
     const uint32_t lane = threadIdx.x & 63u;
     const f3 p00 = mk(p.cam[0], p.cam[1], p.cam[2]);
@@ -386,7 +519,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         // ---- lanes whose item is finished take the next ones (one atomic per wave) ----
         uint64_t need_mask = __ballot(need && !done);
         while (need_mask) {
-            if constexpr (kStats && !kCull) ++st_fetch;
+            if constexpr (kStats && kCull == 0) ++st_fetch;
             const int leader = __ffsll((unsigned long long)need_mask) - 1;
             uint32_t base = 0;
             if ((int)lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need_mask));
@@ -437,7 +570,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         float max_t = 1e5f;
         int best = -1;
         uint32_t hit_groups = 0;
-        if constexpr (kCull) {
+        if constexpr (kCull != 0) {
             // culling needs every ray of the wave in the guarded finite range (see above)
             const float aa = dot(d, d);
             const bool guarded = (p.flags & kFlagSceneBounded) != 0 && aa >= 0x1p-20f &&
@@ -445,8 +578,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(!guarded) == 0) {
                 uint32_t lane_cnt = 0;
-                scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
-                                    lane_cnt);
+                if constexpr (kCull == 1)
+                    scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
+                                        lane_cnt);
+                else
+                    scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
+                                             w_bounds, lane_cnt);
                 if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
                     for (int off = 32; off > 0; off >>= 1)
                         lane_cnt = max(lane_cnt, (uint32_t)__shfl_xor((int)lane_cnt, off));
@@ -583,11 +720,31 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem(TraceParams p)
 
 // Culled scan (exact; see scan_culled): spatially grouped sphere table + wave-level group tests.
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull(TraceParams p) {
-    trace_impl<false, false, true>(p, nullptr);
+    trace_impl<false, false, 1>(p, nullptr);
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_stats(TraceParams p) {
-    trace_impl<false, true, true>(p, nullptr);
+    trace_impl<false, true, 1>(p, nullptr);
+}
+
+// Per-lane culled scan (scan_culled_lane): tables in LDS (dynamic size = group-pair bounds +
+// group records) or read from global memory.
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 2>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, true, 2>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane(TraceParams p) {
+    trace_impl<false, false, 3>(p, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_stats(TraceParams p) {
+    trace_impl<false, true, 3>(p, nullptr);
 }
 
 // Diagnostics builds (VCRT_DEBUG_STATS=1): same kernels plus lane-occupancy/tail counters.
