@@ -12,12 +12,15 @@ import vulkancomputeraytracing_amd as vc  # noqa: E402
 p = argparse.ArgumentParser()
 p.add_argument("--spp", type=int, default=1024)
 p.add_argument("--worlds", default="2,4,8")
+p.add_argument("--chunk", type=int, default=0)
+p.add_argument("--variant", type=int, default=0)
 a = p.parse_args()
-base = dict(width=1920, height=1080, samples_per_pixel=a.spp, max_depth=10, device=0)
+base = dict(width=1920, height=1080, samples_per_pixel=a.spp, max_depth=10, device=0,
+            accumulate_chunk=a.chunk, kernel_variant=a.variant)
 with vc.Renderer(vc.RenderDesc(**base), "final") as r:
     r.draw_next_frame()
     full = r.stats()["kernel_ms"]
-res = {"full_ms": full, "spp": a.spp}
+res = {"full_ms": full, "spp": a.spp, "chunk_arg": a.chunk, "variant": a.variant}
 for world in [int(x) for x in a.worlds.split(",")]:
     per = []
     for rank in range(world):

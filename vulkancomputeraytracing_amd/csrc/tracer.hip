@@ -514,48 +514,60 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     unsigned long long segs = 0;
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
     uint64_t w_groups = 0, w_bounds = 0;  // per wave (uniform): sphere groups / bounds tested
+    // the wave's current block of items (wave-uniform); 64 = exhausted, fetch a new one
+    const uint32_t total_blocks = p.total_items >> 6;
+    uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
 
     for (;;) {
-        // ---- lanes whose item is finished take the next ones (one atomic per wave) ----
+        // ---- lanes whose item is finished take the next slots of the wave's current block
+        //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
         uint64_t need_mask = __ballot(need && !done);
         while (need_mask) {
-            if constexpr (kStats && kCull == 0) ++st_fetch;
-            const int leader = __ffsll((unsigned long long)need_mask) - 1;
-            uint32_t base = 0;
-            if ((int)lane == leader) base = atomicAdd(p.work, (uint32_t)__popcll(need_mask));
-            base = __shfl(base, leader);
-            if (need && !done) {
-                uint32_t item = base + lanes_below(need_mask);
-                if (item >= p.total_items) {
-                    done = true;
-                } else {
-                    if (reverse) item = p.total_items - 1u - item;
-                    // item = (local tile, chunk, slot): 64 consecutive items = one tile x chunk
-                    const uint32_t tile_chunk = item >> 6;
-                    const uint32_t lt = tile_chunk / nchunks;
-                    chunk = tile_chunk - lt * nchunks;
-                    q = lt * 64u + (item & 63u);
-                    const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
-                                              (uint32_t)p.world, (uint32_t)p.rank);
-                    if (px.valid) {
-                        out_index = px.out_index;
-                        // shader.comp:43  pixel00 + x*delta_u + y*delta_v
-                        pc = add(add(p00, scale((float)px.x, du)), scale((float)px.y, dv));
-                        acc = mk(0.f, 0.f, 0.f);
-                        sample = (int)(chunk * (uint32_t)p.chunk);
-                        sample_end = min(sample + p.chunk, p.spp);
-                        // first camera ray of the chunk, shader.comp:48-52
-                        const float2 jt = p.jitter[sample];
-                        const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
-                        o = cam;
-                        d = sub(ps, cam);
-                        atten = mk(1.f, 1.f, 1.f);
-                        pass = 0;
-                        need = false;
-                    }
+            if (blk_next >= 64u) {
+                if constexpr (kStats && kCull == 0) ++st_fetch;
+                const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+                uint32_t b = 0;
+                if ((int)lane == leader) b = atomicAdd(p.work, 1u);
+                b = __builtin_amdgcn_readfirstlane(__shfl(b, leader));
+                if (b >= total_blocks) {  // queue drained: lanes still wanting work are done
+                    if (need) done = true;
+                    break;
+                }
+                if (reverse) b = total_blocks - 1u - b;
+                // block b = (local tile lt, chunk): wave-uniform tile origin and sample range
+                blk_lt = b / nchunks;
+                blk_chunk = b - blk_lt * nchunks;
+                const uint32_t t = blk_lt * (uint32_t)p.world + (uint32_t)p.rank;
+                blk_ty = t / p.tiles_x;
+                blk_tx = t - blk_ty * p.tiles_x;
+                blk_next = 0u;
+            }
+            const uint32_t avail = 64u - blk_next;
+            const uint32_t mine = lanes_below(need_mask);
+            if (need && !done && mine < avail) {
+                const uint32_t slot = blk_next + mine;
+                const uint32_t px = 8u * blk_tx + (slot & 7u), py = 8u * blk_ty + (slot >> 3);
+                if (px < (uint32_t)p.width && py < (uint32_t)p.height) {  // edge tiles: skip
+                    chunk = blk_chunk;
+                    q = blk_lt * 64u + slot;
+                    out_index = p.world == 1 ? py * (uint32_t)p.width + px : q;
+                    // shader.comp:43  pixel00 + x*delta_u + y*delta_v
+                    pc = add(add(p00, scale((float)px, du)), scale((float)py, dv));
+                    acc = mk(0.f, 0.f, 0.f);
+                    sample = (int)(chunk * (uint32_t)p.chunk);
+                    sample_end = min(sample + p.chunk, p.spp);
+                    // first camera ray of the chunk, shader.comp:48-52
+                    const float2 jt = p.jitter[sample];
+                    const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
+                    o = cam;
+                    d = sub(ps, cam);
+                    atten = mk(1.f, 1.f, 1.f);
+                    pass = 0;
+                    need = false;
                 }
             }
-            need_mask = __ballot(need && !done);  // lanes that drew an empty slot retry
+            blk_next += min((uint32_t)__popcll(need_mask), avail);
+            need_mask = __ballot(need && !done);
         }
         const uint64_t live = __ballot(!done);
         if (live == 0) break;
