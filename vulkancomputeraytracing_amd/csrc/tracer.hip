@@ -367,9 +367,16 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
 // large). A wave's work becomes the largest per-lane need instead of the union over lanes.
 // Lanes accept candidates with the same `consider` rule, so the result is the same.
 
-// Per-lane bound test of one pair (any operands): bit 0/1 = this lane may need bound 0/1.
-__device__ __forceinline__ uint32_t bound_pair_bits(const CullRay& r, float4 b0, float4 b1,
-                                                    float2 b2) {
+// (acc << 1) | sign bit of v: v_alignbit_b32, one VALU per collected bit.
+__device__ __forceinline__ uint32_t push_sign(uint32_t acc, float v) {
+    return __builtin_amdgcn_alignbit(acc, __float_as_uint(v), 31);
+}
+
+// Sign of fma(RM, RM, -X) for both bounds of a pair: set (negative) when this lane rules the
+// bound out (X > RM^2 exactly; NaN -- an infinite K at |oC| = 0 -- keeps the default NaN's
+// clear sign bit, i.e. "may need"). Pushed high element first.
+__device__ __forceinline__ uint32_t push_bound_pair(uint32_t acc, const CullRay& r, float4 b0,
+                                                    float4 b1, float2 b2) {
     const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y};
     const v2f K = {b1.z, b1.w}, Rk = {b2.x, b2.y};
     const v2f ocx = r.ox - Cx, ocy = r.oy - Cy, ocz = r.oz - Cz;
@@ -377,8 +384,14 @@ __device__ __forceinline__ uint32_t bound_pair_bits(const CullRay& r, float4 b0,
     const v2f h = vfma(ocz, r.wz, vfma(ocy, r.wy, ocx * r.wx));
     const v2f X = vfma(-h, h, oc2);
     const v2f RM = vfma(K, oc2, Rk);
-    const v2f T = RM * RM;
-    return (uint32_t)!(X.x > T.x) | ((uint32_t)!(X.y > T.y) << 1);
+    const v2f D = vfma(RM, RM, -X);
+    return push_sign(push_sign(acc, D.y), D.x);
+}
+
+// Sign bit set when a member may be accepted: disc >= 0 and (hb < 0 or cc < 0), by sign bits
+// (a -0 hb only adds a candidate that the exact test then rejects; disc is never -0).
+__device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
+    return __uint_as_float((__float_as_uint(hb) | __float_as_uint(cc)) & ~__float_as_uint(disc));
 }
 
 template <bool kStats>
@@ -403,13 +416,15 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
         // level 1, wave-uniform: nodes of this chunk, per-lane bits
         const int nn = min(8, (ncg - base) >> 3);
         cfloat4* nb = node + 3 * (base >> 4);
-        uint32_t nodes = 0;
-        BoundPair cur = load_bound_pair(nb);
-        for (int j = 0; j < nn; j += 2) {
-            const BoundPair nxt = load_bound_pair(nb + 3 * ((j + 2 < nn ? j + 2 : j) >> 1));
-            nodes |= bound_pair_bits(r, cur.b0, cur.b1, cur.b2) << j;
+        // sign bits pushed from the last node down, so bit j ends up = node j ruled out
+        uint32_t out = 0;
+        BoundPair cur = load_bound_pair(nb + 3 * ((nn - 2) >> 1));
+        for (int j = nn - 2; j >= 0; j -= 2) {
+            const BoundPair nxt = load_bound_pair(nb + 3 * ((j >= 2 ? j - 2 : j) >> 1));
+            out = push_bound_pair(out, r, cur.b0, cur.b1, cur.b2);
             cur = nxt;
         }
+        uint32_t nodes = ~out & ((1u << nn) - 1u);
         bounds_tested += (uint64_t)nn;
         // level 2, per lane: the groups of this lane's nodes
         uint64_t need = 0;
@@ -418,14 +433,14 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             if (nodes) {
                 const int j = __builtin_ctz(nodes);
                 nodes &= nodes - 1;
-                const float4* gb = tbound + 3 * ((base + 8 * j) >> 1);
-                uint32_t bits = 0;
+                const float4* gb = tbound + 3 * (base >> 1) + __umul24((uint32_t)j, 12u);
+                uint32_t gout = 0;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
+                for (int k = 3; k >= 0; k--) {
                     const float4 b0 = gb[3 * k], b1 = gb[3 * k + 1], b2 = gb[3 * k + 2];
-                    bits |= bound_pair_bits(r, b0, b1, make_float2(b2.x, b2.y)) << (2 * k);
+                    gout = push_bound_pair(gout, r, b0, b1, make_float2(b2.x, b2.y));
                 }
-                need |= (uint64_t)bits << (8 * j);
+                need |= (uint64_t)(~gout & 0xffu) << (8 * j);
             }
         }
         if constexpr (kStats) lane_cnt += (uint32_t)__popcll(need);
@@ -435,17 +450,18 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             if (need) {
                 const int k = __builtin_ctzll(need);
                 need &= need - 1;
-                const float4* g = tgroup + 5 * (base + k);
+                const float4* g = tgroup + 5 * base + __umul24((uint32_t)k, 5u);
                 const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3], idf = g[4];
                 v2f hb01, cc01, d01, hb23, cc23, d23;
                 pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
                 pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
                 const int i0 = __float_as_int(idf.x), i1 = __float_as_int(idf.y),
                           i2 = __float_as_int(idf.z), i3 = __float_as_int(idf.w);
-                uint32_t hits = (uint32_t)may_hit(hb01.x, cc01.x, d01.x) |
-                                ((uint32_t)may_hit(hb01.y, cc01.y, d01.y) << 1) |
-                                ((uint32_t)may_hit(hb23.x, cc23.x, d23.x) << 2) |
-                                ((uint32_t)may_hit(hb23.y, cc23.y, d23.y) << 3);
+                // bit s = member s may be accepted (sign bits, pushed from member 3 down)
+                uint32_t hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
+                hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
+                hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
+                hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
                 while (hits) {
                     const int s = __builtin_ctz(hits);
                     hits &= hits - 1;

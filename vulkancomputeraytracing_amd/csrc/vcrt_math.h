@@ -144,7 +144,11 @@ VCRT_HD float sin_canonical(float xf) {
 // functions.glsl:10-12  rand(co) = fract(sin(dot(co, vec2(12.9898,78.233))) * 43758.5453)
 VCRT_HD float rand2(float x, float y) {
     float arg = x * 12.9898f + y * 78.233f;
+#ifdef VCRT_EXPERIMENT_FAST_SIN  // timing experiments only: not the canonical value
+    float p = __builtin_sinf(arg) * 43758.5453f;
+#else
     float p = sin_canonical(arg) * 43758.5453f;
+#endif
     return p - __builtin_floorf(p);
 }
 
