@@ -177,6 +177,10 @@ def test_bound_test_is_conservative(name):
         node_culled = np.repeat(group_culled(t, o, d, "node", rng=rng), 8, axis=1)
         bad = node_culled[:, :, None] & hit
         assert not bad.any(), f"{int(bad.sum())} culled node members with disc >= 0"
+        G = hit.shape[1]
+        top_culled = np.repeat(group_culled(t, o, d, "top", rng=rng), 64, axis=1)[:, :G]
+        bad = top_culled[:, :, None] & hit
+        assert not bad.any(), f"{int(bad.sum())} culled top-level members with disc >= 0"
         total_culled += int(culled.sum())
         total += culled.size
     # and the test does cull (most groups are far from most rays)

@@ -66,6 +66,7 @@ struct RendererState {
     float4* d_cgroup = nullptr;
     float4* d_cbound = nullptr;
     float4* d_cnode = nullptr;
+    float4* d_ctop = nullptr;
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
     uint32_t total_pixels = 0, total_items = 0;
@@ -160,9 +161,11 @@ void free_scene() {
     if (g.d_cgroup) (void)hipFree(g.d_cgroup);
     if (g.d_cbound) (void)hipFree(g.d_cbound);
     if (g.d_cnode) (void)hipFree(g.d_cnode);
+    if (g.d_ctop) (void)hipFree(g.d_ctop);
     g.d_cgroup = nullptr;
     g.d_cbound = nullptr;
     g.d_cnode = nullptr;
+    g.d_ctop = nullptr;
     g.ncgroups = 0;
     g.nspheres = 0;
 }
@@ -419,6 +422,9 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         VCRT_TRY(hipMalloc(&g.d_cgroup, sizeof(float) * rec.size()));
         VCRT_TRY(hipMalloc(&g.d_cbound, sizeof(float) * ct.bound.size()));
         VCRT_TRY(hipMalloc(&g.d_cnode, sizeof(float) * ct.node.size()));
+        VCRT_TRY(hipMalloc(&g.d_ctop, sizeof(float) * ct.top.size()));
+        VCRT_TRY(hipMemcpy(g.d_ctop, ct.top.data(), sizeof(float) * ct.top.size(),
+                           hipMemcpyHostToDevice));
         VCRT_TRY(hipMemcpy(g.d_cgroup, rec.data(), sizeof(float) * rec.size(),
                            hipMemcpyHostToDevice));
         VCRT_TRY(hipMemcpy(g.d_cbound, ct.bound.data(), sizeof(float) * ct.bound.size(),
@@ -493,6 +499,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.cgroup = g.d_cgroup;
         p.cbound = g.d_cbound;
         p.cnode = g.d_cnode;
+        p.ctop = g.d_ctop;
         p.ncgroups = g.ncgroups;
         p.nspheres = g.nspheres;
         p.width = g.desc.width;
@@ -760,7 +767,7 @@ size_t vcrt_scene_generator_text(char* buf, size_t cap) {
 }
 
 int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
-                         float* node, int32_t* index, int32_t cap_groups) {
+                         float* node, float* top, int32_t* index, int32_t cap_groups) {
     if (count < 0 || (count > 0 && !spheres)) return 0;
     vcrt::CullTables ct;
     if (!vcrt::build_cull_tables(spheres, count, ct)) return 0;
@@ -768,6 +775,7 @@ int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom,
         if (geom) std::memcpy(geom, ct.geom.data(), sizeof(float) * ct.geom.size());
         if (bound) std::memcpy(bound, ct.bound.data(), sizeof(float) * ct.bound.size());
         if (node) std::memcpy(node, ct.node.data(), sizeof(float) * ct.node.size());
+        if (top) std::memcpy(top, ct.top.data(), sizeof(float) * ct.top.size());
         if (index) std::memcpy(index, ct.index.data(), sizeof(int32_t) * ct.index.size());
     }
     return ct.ngroups;

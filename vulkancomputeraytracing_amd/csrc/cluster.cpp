@@ -184,6 +184,16 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
     }
     for (size_t gi = 0; gi < ng; gi++) put_bound(out.bound, gi, gb[gi]);
     for (size_t ni = 0; ni < nb.size(); ni++) put_bound(out.node, ni, nb[ni]);
+    // top level: one bound per chunk of 64 groups (the kernels' unit of work per pass)
+    const size_t nt = (ng + 63) / 64, nt2 = nt + (nt & 1);
+    out.top.assign(nt2 / 2 * 12, 0.0f);
+    for (size_t ti = 0; ti < nt2; ti++) {
+        std::vector<int32_t> members;
+        for (size_t gi = ti * 64; gi < std::min(ng, ti * 64 + 64); gi++)
+            for (int k = 0; k < 4; k++)
+                if (groups[gi][k] >= 0) members.push_back(groups[gi][k]);
+        put_bound(out.top, ti, bound_of(s, members));
+    }
     return true;
 }
 

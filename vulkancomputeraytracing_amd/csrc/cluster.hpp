@@ -20,6 +20,8 @@ struct CullTables {
     std::vector<float> geom;      // [ngroups][16] pair-SoA, same values as the linear table
     std::vector<float> bound;     // [ngroups / 2][12] group-pair bounds (TraceParams.cbound)
     std::vector<float> node;      // [ngroups / kNodeGroups / 2][12] node-pair bounds, same form
+    std::vector<float> top;       // [ceil(ngroups / 64) rounded up to even / 2][12] bounds of
+                                  // each 64-group chunk (8 nodes), same form
     std::vector<int32_t> index;   // [ngroups][4] world[] index of each member, -1 = padding
 };
 

@@ -293,7 +293,16 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* geom = (cfloat4*)p.cgroup;
     const int ncg = p.ncgroups;  // multiple of 16: whole node pairs
+    cfloat4* top = (cfloat4*)p.ctop;
+    uint32_t tops = 0;
     for (int base = 0; base < ncg; base += 64) {
+        // level 0: the chunk's own bound (tested for two chunks at a time)
+        if ((base & 127) == 0) {
+            tops = bound_pair_need<false>(r, load_bound_pair(top + 3 * (base >> 7)), node_lanes,
+                                          node_cnt);
+            bounds_tested += 2;
+        }
+        if (((tops >> ((base >> 6) & 1)) & 1u) == 0) continue;
         // level 1: which of the next (up to) 8 nodes of 8 groups may any lane hit? (the
         // scalar loads run one pair ahead of the tests)
         const int nn = min(8, (ncg - base) >> 3);
@@ -411,8 +420,18 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
     r.wz = (v2f){d.z * inv, d.z * inv};
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     cfloat4* node = (cfloat4*)p.cnode;
+    cfloat4* top = (cfloat4*)p.ctop;
     const int ncg = p.ncgroups;
+    uint32_t tops = 0;
     for (int base = 0; base < ncg; base += 64) {
+        // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
+        if ((base & 127) == 0) {
+            const BoundPair tp = load_bound_pair(top + 3 * (base >> 7));
+            tops = ~push_bound_pair(0u, r, tp.b0, tp.b1, tp.b2) & 3u;
+            bounds_tested += 2;
+        }
+        const bool in_chunk = ((tops >> ((base >> 6) & 1)) & 1u) != 0;
+        if (__ballot(in_chunk) == 0) continue;
         // level 1, wave-uniform: nodes of this chunk, per-lane bits
         const int nn = min(8, (ncg - base) >> 3);
         cfloat4* nb = node + 3 * (base >> 4);
@@ -424,7 +443,7 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             out = push_bound_pair(out, r, cur.b0, cur.b1, cur.b2);
             cur = nxt;
         }
-        uint32_t nodes = ~out & ((1u << nn) - 1u);
+        uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
         bounds_tested += (uint64_t)nn;
         // level 2, per lane: the groups of this lane's nodes
         uint64_t need = 0;

@@ -37,6 +37,7 @@ struct TraceParams {
     const float4* cbound;   // [ncgroups / 2 * 3] bounds of group pairs, pair-SoA:
                             //   (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1) (Rk0,Rk1,0,0), tracer.hip
     const float4* cnode;    // [ncgroups / 16 * 3] bounds of node pairs (8 groups per node)
+    const float4* ctop;     // bounds of pairs of 64-group chunks, same form
     int32_t ncgroups;       // multiple of 16
     int32_t nspheres;
     int32_t width, height, spp, max_depth;
