@@ -184,18 +184,21 @@ def main():
         value = samples / elapsed / 1e6
         k_ms = sum(kernel_ms) / len(kernel_ms)
         seg = sum(segments) / len(segments)
+        # Reference-equivalent work: the reference's linear scan tests every sphere on every
+        # segment (segments x spheres x 23 flops).
         flops = seg * nspheres * FLOPS_PER_SPHERE_TEST
-        achieved = flops / (k_ms * 1e-3) / 1e12
-        # The culled scan skips most of the reference's per-segment sphere tests (same bits),
-        # so the algorithmic rate above counts work it never issued; the flops it did issue
-        # (every lane of each wave-level group test and bound test) bound the VALU side.
-        executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
-                    + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
-        if st["kernel_variant"] not in (3, 4):
-            executed = flops
+        # Issued work: the culled scans skip most of those tests (same bits), so the roofline
+        # numerator is what the kernel actually issued -- every lane of each wave-level group
+        # test (4 spheres x 23) and bound test (18) -- which is all there is for the linear scan.
+        executed = flops
+        if st["kernel_variant"] in (3, 4):
+            executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
+                        + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
         kernel = KERNEL_NAMES.get(st["kernel_variant"], "?")
         if st["kernel_variant"] == 4 and st["lds_bytes"] > 0:
             kernel += "_lds"
+        achieved = executed / (k_ms * 1e-3) / 1e12
+        equivalent = flops / (k_ms * 1e-3) / 1e12
         traffic = None
         if os.path.exists(PROFILE_TRAFFIC):
             try:
@@ -229,14 +232,14 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": traffic,
-                         "kernel": kernel,
-                         "kernel_ms": round(k_ms, 3), "segments_per_launch": int(seg),
-                         "flops_per_launch": flops,
-                         "numerator": "algorithmic: segments x spheres x 23 (SURVEY 8(d))",
-                         "executed_flops_per_launch": executed,
-                         "executed_tflops": round(executed / (k_ms * 1e-3) / 1e12, 3),
-                         "executed_frac": round(executed / (k_ms * 1e-3) / 1e12
-                                                / PEAK_FP32_TFLOPS, 4)},
+                         "kernel": kernel, "kernel_ms": round(k_ms, 3),
+                         "numerator": "issued sphere-test and bound-test flops per launch "
+                                      "(DESIGN.md 5): wave-level group tests x 64 x 4 x 23 + "
+                                      "bound tests x 64 x 18",
+                         "flops_per_launch": executed,
+                         "segments_per_launch": int(seg),
+                         "reference_equivalent_flops_per_launch": flops,
+                         "reference_equivalent_tflops": round(equivalent, 3)},
         }
         if validated is not None:
             out["validated_bitwise_vs_1gpu"] = validated
