@@ -45,8 +45,8 @@ def group_culled(t, o, d, key="bound", rng=None):
 
 
 def member_disc(t, o, d):
-    """[rays, groups, 4] fp32 discriminants exactly as pair_disc computes them."""
-    g = t["geom"]
+    """[rays, hierarchy groups, 4] fp32 discriminants exactly as pair_disc computes them."""
+    g = t["geom"][t["nbig"]:]
     cx = np.stack([g[:, 0], g[:, 1], g[:, 8], g[:, 9]], 1)
     cy = np.stack([g[:, 2], g[:, 3], g[:, 10], g[:, 11]], 1)
     cz = np.stack([g[:, 4], g[:, 5], g[:, 12], g[:, 13]], 1)
@@ -87,11 +87,12 @@ def tangent_rays(spheres, t, n, rng):
     """Rays tangent to a group's outermost member on the side facing away from the group
     centre: they graze the member where it touches the bounding sphere (the tightest case for
     the bound test)."""
-    G = t["geom"].shape[0]
+    G = t["geom"].shape[0] - t["nbig"]
     os_, ds_ = [], []
     for gi in rng.integers(0, G, n):
         C = bound_of(t, gi)
-        m = t["index"][gi][t["index"][gi] >= 0]
+        idx = t["index"][t["nbig"] + gi]
+        m = idx[idx >= 0]
         if len(m) == 0:
             continue
         c = spheres["center"][m].astype(np.float64)
@@ -119,13 +120,19 @@ def test_groups_partition_the_scene(name):
     sp = S.builtin_scene(name)
     t = S.cull_tables(sp)
     assert t is not None
-    G = t["geom"].shape[0]
-    assert G % 16 == 0 and G >= (len(sp) + 3) // 4 and t["node"].shape[0] == G // 16
+    nb = t["nbig"]
+    G = t["geom"].shape[0] - nb
+    assert G % 16 == 0 and t["node"].shape[0] == G // 16 and t["bound"].shape[0] == G // 2
     idx = t["index"].reshape(-1)
     members = np.sort(idx[idx >= 0])
     assert np.array_equal(members, np.arange(len(sp)))
+    # the big-sphere list holds exactly the spheres above 8x the median radius
+    r = np.abs(sp["radius"])
+    big = set(np.nonzero(r > 8 * np.partition(r, len(r) // 2)[len(r) // 2])[0].tolist())
+    bi = t["index"][:nb].reshape(-1)
+    assert set(bi[bi >= 0].tolist()) == big
     g = t["geom"]
-    for gi in range(G):
+    for gi in range(nb + G):
         for k in range(4):
             j = t["index"][gi, k]
             if j < 0:
@@ -135,18 +142,16 @@ def test_groups_partition_the_scene(name):
             assert g[gi, base + 2] == sp["center"][j, 1]
             assert g[gi, base + 4] == sp["center"][j, 2]
             assert g[gi, base + 6] == f32(sp["radius"][j]) * f32(sp["radius"][j])
-            # bound covers the member: Rk >= R (float64 geometry)
-            e = gi % 2
-            b = t["bound"][gi // 2]
-            C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
-            dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
-            assert dist + abs(float(sp["radius"][j])) <= float(b[8 + e])
-            # and so does its node's
-            ni = gi // 8
-            e, b = ni % 2, t["node"][ni // 2]
-            C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
-            dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
-            assert dist + abs(float(sp["radius"][j])) <= float(b[8 + e])
+            if gi < nb:
+                continue
+            h = gi - nb
+            # the bound covers the member: Rk >= R (float64 geometry), and so do the node's
+            # and the chunk's
+            for tab, i in (("bound", h), ("node", h // 8), ("top", h // 64)):
+                e, b = i % 2, t[tab][i // 2]
+                C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
+                dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
+                assert dist + abs(float(sp["radius"][j])) <= float(b[8 + e]), (tab, i)
 
 
 def test_small_or_unbounded_scenes_do_not_cull():
@@ -161,7 +166,7 @@ def test_bound_test_is_conservative(name):
     rng = np.random.default_rng(7)
     sp = S.builtin_scene(name)
     t = S.cull_tables(sp)
-    valid = t["index"] >= 0
+    valid = t["index"][t["nbig"]:] >= 0
     total_culled = 0
     total = 0
     chunks = [grazing_rays(sp, 1500, rng) for _ in range(3)]
@@ -192,12 +197,12 @@ def test_checker_detects_a_too_small_bound():
     rng = np.random.default_rng(11)
     sp = S.builtin_scene("final")
     t = S.cull_tables(sp)
-    bad_t = {k: v.copy() for k, v in t.items()}
+    bad_t = {k: (v.copy() if hasattr(v, "copy") else v) for k, v in t.items()}
     bad_t["bound"][:, 6:8] = 0                   # no margin
     bad_t["bound"][:, 8:10] *= f32(0.99)         # radius 1% short
     o, d = tangent_rays(sp, t, 1500, rng)
     culled = group_culled(bad_t, o, d)
-    hit = ~(member_disc(t, o, d) < 0) & (t["index"] >= 0)[None]
+    hit = ~(member_disc(t, o, d) < 0) & (t["index"][t["nbig"]:] >= 0)[None]
     assert (culled[:, :, None] & hit).any()
 
 
@@ -207,8 +212,9 @@ def test_margin_constants():
     sp = S.builtin_scene("final")
     t = S.cull_tables(sp)
     u = 2.0 ** -24
-    for gi in range(t["geom"].shape[0]):
-        m = t["index"][gi][t["index"][gi] >= 0]
+    nb = t["nbig"]
+    for gi in range(t["geom"].shape[0] - nb):
+        m = t["index"][nb + gi][t["index"][nb + gi] >= 0]
         if len(m) == 0:
             continue
         e, bb = gi % 2, t["bound"][gi // 2]
@@ -218,3 +224,15 @@ def test_margin_constants():
         Kc = 32.4 * u / r.min()
         assert float(bb[6 + e]) >= Kc * (1 + 1e-5) + 6e-6 / (2 * R * (1 + 1e-6))
         assert float(bb[8 + e]) >= (R + 1.5 * Kc * R * R) * (1 + 1e-5)
+
+
+def test_hierarchy_is_aligned():
+    """Nodes (8 groups) and chunks (64 groups) are whole k-d subtrees: a node's bound is no
+    larger than the union of its groups' bounds needs (sanity: node radius <= 4x median group
+    radius on the grid scenes)."""
+    for name in ("final", "stress4096"):
+        t = S.cull_tables(S.builtin_scene(name))
+        gR = np.concatenate([t["bound"][:, 8], t["bound"][:, 9]])
+        nR = np.concatenate([t["node"][:, 8], t["node"][:, 9]])
+        real = nR > 0
+        assert np.median(nR[real]) <= 4 * np.median(gR[gR > 0])

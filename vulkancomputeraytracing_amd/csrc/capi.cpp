@@ -62,7 +62,7 @@ struct RendererState {
     float4* d_shade = nullptr;
     float* d_material = nullptr;
     // culled-scan tables (cluster.hpp); ncgroups == 0 when culling does not apply
-    int32_t ncgroups = 0;
+    int32_t ncgroups = 0, ncbig = 0;
     float4* d_cgroup = nullptr;
     float4* d_cbound = nullptr;
     float4* d_cnode = nullptr;
@@ -167,6 +167,7 @@ void free_scene() {
     g.d_cnode = nullptr;
     g.d_ctop = nullptr;
     g.ncgroups = 0;
+    g.ncbig = 0;
     g.nspheres = 0;
 }
 
@@ -414,8 +415,9 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     free_scene();
     if (ct.ngroups > 0) {
         // group records: the four pair-SoA float4s + the member indices (int bits)
-        std::vector<float> rec(static_cast<size_t>(ct.ngroups) * 20);
-        for (int32_t gi = 0; gi < ct.ngroups; gi++) {
+        const int32_t nall = ct.nbig + ct.ngroups;  // big-sphere groups first
+        std::vector<float> rec(static_cast<size_t>(nall) * 20);
+        for (int32_t gi = 0; gi < nall; gi++) {
             std::memcpy(&rec[gi * 20], &ct.geom[gi * 16], 16 * sizeof(float));
             std::memcpy(&rec[gi * 20 + 16], &ct.index[gi * 4], 4 * sizeof(int32_t));
         }
@@ -432,6 +434,7 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         VCRT_TRY(hipMemcpy(g.d_cnode, ct.node.data(), sizeof(float) * ct.node.size(),
                            hipMemcpyHostToDevice));
         g.ncgroups = ct.ngroups;
+        g.ncbig = ct.nbig;
     }
     VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float) * table.size()));
     VCRT_TRY(hipMemcpy(g.d_geom, table.data(), sizeof(float) * table.size(),
@@ -501,6 +504,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.cnode = g.d_cnode;
         p.ctop = g.d_ctop;
         p.ncgroups = g.ncgroups;
+        p.nbig = g.ncbig;
         p.nspheres = g.nspheres;
         p.width = g.desc.width;
         p.height = g.desc.height;
@@ -767,11 +771,13 @@ size_t vcrt_scene_generator_text(char* buf, size_t cap) {
 }
 
 int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
-                         float* node, float* top, int32_t* index, int32_t cap_groups) {
+                         float* node, float* top, int32_t* index, int32_t* big_groups,
+                         int32_t cap_groups) {
     if (count < 0 || (count > 0 && !spheres)) return 0;
     vcrt::CullTables ct;
     if (!vcrt::build_cull_tables(spheres, count, ct)) return 0;
-    if (ct.ngroups <= cap_groups) {
+    if (big_groups) *big_groups = ct.nbig;
+    if (ct.nbig + ct.ngroups <= cap_groups) {
         if (geom) std::memcpy(geom, ct.geom.data(), sizeof(float) * ct.geom.size());
         if (bound) std::memcpy(bound, ct.bound.data(), sizeof(float) * ct.bound.size());
         if (node) std::memcpy(node, ct.node.data(), sizeof(float) * ct.node.size());

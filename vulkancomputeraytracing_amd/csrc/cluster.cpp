@@ -18,8 +18,10 @@ float round_up(double x) {
 
 using Group = std::array<int32_t, 4>;
 
-// Median splits on the widest centre axis; the left part always holds a multiple of four
-// spheres so only the last leaf of a run is padded.
+// Median splits on the widest centre axis. The left part gets ceil(groups / 2) groups rounded
+// up to a multiple of 64 (more than 64 groups) or 8 (more than 8), so every subtree starts on a
+// node (8 groups) and chunk (64 groups) boundary and nodes are whole subtrees; only the last
+// leaf is partial.
 void split(std::vector<int32_t>& idx, size_t lo, size_t hi, const vcrt_sphere* s,
            std::vector<Group>& groups) {
     const size_t n = hi - lo;
@@ -43,7 +45,9 @@ void split(std::vector<int32_t>& idx, size_t lo, size_t hi, const vcrt_sphere* s
     for (int a = 1; a < 3; a++)
         if (mx[a] - mn[a] > mx[axis] - mn[axis]) axis = a;
     const size_t ng = (n + 3) / 4;
-    const size_t mid = lo + 4 * ((ng + 1) / 2);
+    const size_t align = ng > 64 ? 64 : ng > 8 ? 8 : 1;
+    const size_t left = ((ng + 1) / 2 + align - 1) / align * align;
+    const size_t mid = lo + 4 * left;
     std::nth_element(idx.begin() + lo, idx.begin() + mid, idx.begin() + hi,
                      [&](int32_t x, int32_t y) {
                          const float cx = s[x].center[axis], cy = s[y].center[axis];
@@ -136,22 +140,23 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
     const float huge = 8.0f * sorted[count / 2];
     std::vector<int32_t> normal, big;
     for (int32_t i = 0; i < count; i++) (radii[i] > huge ? big : normal).push_back(i);
-    // Big spheres first, in groups of their own.
-    std::vector<Group> groups;
-    if (!big.empty()) split(big, 0, big.size(), s, groups);
+    // Big spheres go to a short list the kernels test for every ray (they are hit by most);
+    // the rest form the hierarchy: groups of 4, nodes of 8 groups, chunks of 64 groups.
+    std::vector<Group> bigg, groups;
+    if (!big.empty()) split(big, 0, big.size(), s, bigg);
     if (!normal.empty()) split(normal, 0, normal.size(), s, groups);
-    // pad to whole nodes of kNodeGroups groups, and to an even node count (pair layout)
+    // pad the hierarchy to whole nodes and an even node count (pair layout)
     while (groups.size() % (2 * kNodeGroups)) groups.push_back(Group{-1, -1, -1, -1});
 
-    const size_t ng = groups.size();
+    const size_t nbig = bigg.size(), ng = groups.size(), nall = nbig + ng;
+    out.nbig = static_cast<int32_t>(nbig);
     out.ngroups = static_cast<int32_t>(ng);
-    out.geom.assign(ng * 16, 0.0f);
+    out.geom.assign(nall * 16, 0.0f);
+    out.index.assign(nall * 4, -1);
     out.bound.assign(ng / 2 * 12, 0.0f);
     out.node.assign(ng / kNodeGroups / 2 * 12, 0.0f);
-    out.index.assign(ng * 4, -1);
-    std::vector<Bound> gb(ng), nb(ng / kNodeGroups);
-    for (size_t gi = 0; gi < ng; gi++) {
-        const Group& g = groups[gi];
+    for (size_t gi = 0; gi < nall; gi++) {
+        const Group& g = gi < nbig ? bigg[gi] : groups[gi - nbig];
         // members: pair-SoA exactly as the linear table (r^2 = radius * radius in fp32)
         for (int k = 0; k < 4; k++) {
             float* base = &out.geom[gi * 16 + 8 * (k / 2)];
@@ -170,30 +175,21 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
             base[6 + e] = r2;
             out.index[gi * 4 + k] = g[k];
         }
-        std::vector<int32_t> members;
-        for (int k = 0; k < 4; k++)
-            if (g[k] >= 0) members.push_back(g[k]);
-        gb[gi] = bound_of(s, members);
     }
-    for (size_t ni = 0; ni < nb.size(); ni++) {
-        std::vector<int32_t> members;
-        for (size_t gi = ni * kNodeGroups; gi < (ni + 1) * kNodeGroups; gi++)
+    auto members_of = [&](size_t g0, size_t g1) {
+        std::vector<int32_t> m;
+        for (size_t gi = g0; gi < std::min(g1, ng); gi++)
             for (int k = 0; k < 4; k++)
-                if (groups[gi][k] >= 0) members.push_back(groups[gi][k]);
-        nb[ni] = bound_of(s, members);
-    }
-    for (size_t gi = 0; gi < ng; gi++) put_bound(out.bound, gi, gb[gi]);
-    for (size_t ni = 0; ni < nb.size(); ni++) put_bound(out.node, ni, nb[ni]);
+                if (groups[gi][k] >= 0) m.push_back(groups[gi][k]);
+        return m;
+    };
+    for (size_t gi = 0; gi < ng; gi++) put_bound(out.bound, gi, bound_of(s, members_of(gi, gi + 1)));
+    for (size_t ni = 0; ni < ng / kNodeGroups; ni++)
+        put_bound(out.node, ni, bound_of(s, members_of(ni * kNodeGroups, (ni + 1) * kNodeGroups)));
     // top level: one bound per chunk of 64 groups (the kernels' unit of work per pass)
     const size_t nt = (ng + 63) / 64, nt2 = nt + (nt & 1);
     out.top.assign(nt2 / 2 * 12, 0.0f);
-    for (size_t ti = 0; ti < nt2; ti++) {
-        std::vector<int32_t> members;
-        for (size_t gi = ti * 64; gi < std::min(ng, ti * 64 + 64); gi++)
-            for (int k = 0; k < 4; k++)
-                if (groups[gi][k] >= 0) members.push_back(groups[gi][k]);
-        put_bound(out.top, ti, bound_of(s, members));
-    }
+    for (size_t ti = 0; ti < nt2; ti++) put_bound(out.top, ti, bound_of(s, members_of(ti * 64, ti * 64 + 64)));
     return true;
 }
 

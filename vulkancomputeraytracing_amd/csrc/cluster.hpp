@@ -16,13 +16,14 @@ namespace vcrt {
 constexpr int kNodeGroups = 8;  // groups per node of the bound hierarchy
 
 struct CullTables {
-    int32_t ngroups = 0;          // a multiple of 2 * kNodeGroups (padded with empty groups)
-    std::vector<float> geom;      // [ngroups][16] pair-SoA, same values as the linear table
-    std::vector<float> bound;     // [ngroups / 2][12] group-pair bounds (TraceParams.cbound)
+    int32_t nbig = 0;             // big-sphere groups, first in geom/index, tested for every ray
+    int32_t ngroups = 0;          // hierarchy groups after them, a multiple of 2 * kNodeGroups
+    std::vector<float> geom;      // [nbig + ngroups][16] pair-SoA, same values as the linear table
+    std::vector<int32_t> index;   // [nbig + ngroups][4] world[] index of each member, -1 = padding
+    std::vector<float> bound;     // [ngroups / 2][12] hierarchy group-pair bounds (TraceParams)
     std::vector<float> node;      // [ngroups / kNodeGroups / 2][12] node-pair bounds, same form
     std::vector<float> top;       // [ceil(ngroups / 64) rounded up to even / 2][12] bounds of
                                   // each 64-group chunk (8 nodes), same form
-    std::vector<int32_t> index;   // [ngroups][4] world[] index of each member, -1 = padding
 };
 
 // Builds the grouped tables. Returns false (tables empty) when culling does not apply: fewer

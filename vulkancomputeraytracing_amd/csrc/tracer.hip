@@ -271,6 +271,29 @@ __device__ __forceinline__ uint32_t bound_pair_need(const CullRay& r, const Boun
     return nonzero(n0) | (nonzero(n1) << 1);
 }
 
+// The exact test of one group for every lane (wave-uniform scalar loads of the 80-B record):
+// the big-sphere list, tested for every ray ahead of the hierarchy.
+__device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay& r, v2f dx, v2f dy,
+                                                    v2f dz, v2f a2, float a, float& max_t,
+                                                    int& best) {
+    const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
+    v2f hb01, cc01, d01, hb23, cc23, d23;
+    pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+    pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+    const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
+    if (__ballot(!(m4 < 0.0f))) {
+        const float4 idf = rec[4];
+        if (may_hit(hb01.x, cc01.x, d01.x))
+            consider(candidate_t(hb01.x, d01.x, a), __float_as_int(idf.x), max_t, best);
+        if (may_hit(hb01.y, cc01.y, d01.y))
+            consider(candidate_t(hb01.y, d01.y, a), __float_as_int(idf.y), max_t, best);
+        if (may_hit(hb23.x, cc23.x, d23.x))
+            consider(candidate_t(hb23.x, d23.x, a), __float_as_int(idf.z), max_t, best);
+        if (may_hit(hb23.y, cc23.y, d23.y))
+            consider(candidate_t(hb23.y, d23.y, a), __float_as_int(idf.w), max_t, best);
+    }
+}
+
 // Stats builds count in `hit_groups` the lanes that need each group (sum over group bounds)
 // and in `lane_cnt` the groups this lane needs.
 template <bool kStats>
@@ -292,6 +315,10 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     cfloat4* bound = (cfloat4*)p.cbound;
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* geom = (cfloat4*)p.cgroup;
+    for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray
+        exact_group_uniform(geom + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
+    groups_tested += (uint64_t)p.nbig;
+    geom += 5 * p.nbig;           // the hierarchy's groups
     const int ncg = p.ncgroups;  // multiple of 16: whole node pairs
     cfloat4* top = (cfloat4*)p.ctop;
     uint32_t tops = 0;
@@ -408,7 +435,8 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
                                                  const float4* tgroup, const f3 o, const f3 d,
                                                  float& max_t, int& best,
                                                  uint64_t& groups_tested,
-                                                 uint64_t& bounds_tested, uint32_t& lane_cnt) {
+                                                 uint64_t& bounds_tested, uint32_t& lane_cnt,
+                                                 uint32_t& rounds) {
     const float a = dot(d, d);
     const float inv = __builtin_amdgcn_rsqf(a);
     CullRay r;
@@ -422,6 +450,9 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* top = (cfloat4*)p.ctop;
     const int ncg = p.ncgroups;
+    for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
+        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
+    groups_tested += (uint64_t)p.nbig;
     uint32_t tops = 0;
     for (int base = 0; base < ncg; base += 64) {
         // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
@@ -466,6 +497,7 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
         // the exact test, per lane on its own groups
         while (__ballot(need != 0)) {
             ++groups_tested;
+            uint32_t cand = 0;  // stats: candidate roots this lane evaluates in this pass
             if (need) {
                 const int k = __builtin_ctzll(need);
                 need &= need - 1;
@@ -481,6 +513,7 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
                 hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
                 hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
                 hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
+                if constexpr (kStats) cand = __popc(hits);
                 while (hits) {
                     const int s = __builtin_ctz(hits);
                     hits &= hits - 1;
@@ -489,6 +522,11 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
                     const int idx = s == 0 ? i0 : s == 1 ? i1 : s == 2 ? i2 : i3;
                     consider(candidate_t(hb, ds, a), idx, max_t, best);
                 }
+            }
+            if constexpr (kStats) {  // wave passes of the candidate loop = max over lanes
+                for (int off = 32; off > 0; off >>= 1)
+                    cand = max(cand, (uint32_t)__shfl_xor((int)cand, off));
+                rounds += cand;
             }
         }
     }
@@ -524,11 +562,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         __syncthreads();
     }
     const float4* tbound = p.cbound;
-    const float4* tgroup = p.cgroup;
+    const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
     if constexpr (kCull == 2) {
         const int nb = (p.ncgroups >> 1) * 3, ng = p.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = p.cbound[i];
-        for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = p.cgroup[i];
+        for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = tgroup[i];
         __syncthreads();
         tbound = lds_geom;
         tgroup = lds_geom + nb;
@@ -630,7 +668,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                                         lane_cnt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
-                                             w_bounds, lane_cnt);
+                                             w_bounds, lane_cnt, hit_groups);
                 if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
                     for (int off = 32; off > 0; off >>= 1)
                         lane_cnt = max(lane_cnt, (uint32_t)__shfl_xor((int)lane_cnt, off));

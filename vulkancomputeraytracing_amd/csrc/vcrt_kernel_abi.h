@@ -31,14 +31,16 @@ struct TraceParams {
     unsigned long long* debug;     // diagnostics counters (stats kernels only), may be null
     unsigned long long* work_done;  // [2]: sphere groups tested, group bounds tested
     // spatially clustered copy of the scene for the culled scan (kernel variant CULL)
-    const float4* cgroup;   // [ncgroups * 5] per group: four pair-SoA float4s (cx0,cx1,cy0,cy1)
-                            //   (cz0,cz1,r0^2,r1^2) (cx2..) (cz2..) + the members' world[]
-                            //   indices as int bits (-1 = padding); spatial order
+    const float4* cgroup;   // [(nbig + ncgroups) * 5] per group: four pair-SoA float4s
+                            //   (cx0,cx1,cy0,cy1) (cz0,cz1,r0^2,r1^2) (cx2..) (cz2..) + the
+                            //   members' world[] indices as int bits (-1 = padding); the nbig
+                            //   big-sphere groups first, then the hierarchy in spatial order
     const float4* cbound;   // [ncgroups / 2 * 3] bounds of group pairs, pair-SoA:
                             //   (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1) (Rk0,Rk1,0,0), tracer.hip
     const float4* cnode;    // [ncgroups / 16 * 3] bounds of node pairs (8 groups per node)
     const float4* ctop;     // bounds of pairs of 64-group chunks, same form
-    int32_t ncgroups;       // multiple of 16
+    int32_t ncgroups;       // hierarchy groups, multiple of 16
+    int32_t nbig;           // big-sphere groups tested for every ray
     int32_t nspheres;
     int32_t width, height, spp, max_depth;
     int32_t rank, world;
