@@ -535,14 +535,12 @@ vcrt_result vcrt_draw_next_frame(void) {
         int variant = g.desc.kernel_variant;
         // Measured on MI355X: of the linear scans the scalar-cache variant (sphere data in
         // SGPRs, no LDS traffic) beats LDS staging by 15% (485 spheres) and 18% (4100); the
-        // culled scans beat both (same bits). AUTO: the per-lane culled scan when its tables
-        // fit in LDS (485 spheres: +46% over SMEM, +10% over CULL), else the wave-uniform
-        // culled scan (4100 spheres: +75% over SMEM; per-lane on global tables is ~5% slower),
-        // and SMEM when the scene has no tables (< 16 spheres or unbounded).
+        // culled scans beat both (same bits). AUTO: the per-lane culled scan (485 spheres,
+        // tables in LDS: 2.5x SMEM, +27% over CULL; 4100 spheres, tables in global memory:
+        // 1.9x SMEM, +4% over CULL), and SMEM when the scene has no tables (< 16 spheres or
+        // unbounded).
         if (variant == VCRT_KERNEL_AUTO)
-            variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM
-                      : lane_lds      ? VCRT_KERNEL_CULL_LANE
-                                      : VCRT_KERNEL_CULL;
+            variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_LANE;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
         if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE) &&
             g.ncgroups == 0)
