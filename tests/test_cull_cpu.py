@@ -126,9 +126,13 @@ def test_groups_partition_the_scene(name):
     idx = t["index"].reshape(-1)
     members = np.sort(idx[idx >= 0])
     assert np.array_equal(members, np.arange(len(sp)))
-    # the big-sphere list holds exactly the spheres above 8x the median radius
-    r = np.abs(sp["radius"])
-    big = set(np.nonzero(r > 8 * np.partition(r, len(r) // 2)[len(r) // 2])[0].tolist())
+    # the big-sphere list holds exactly the spheres above 8x the median radius and 5% of the
+    # extent of the centres (at most 64)
+    r = np.abs(sp["radius"]).astype(np.float64)
+    c = sp["center"].astype(np.float64)
+    extent = np.linalg.norm(c.max(0) - c.min(0))
+    huge = max(8 * np.partition(r, len(r) // 2)[len(r) // 2], 0.05 * extent)
+    big = set(np.nonzero(r > huge)[0].tolist())
     bi = t["index"][:nb].reshape(-1)
     assert set(bi[bi >= 0].tolist()) == big
     g = t["geom"]

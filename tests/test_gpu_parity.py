@@ -156,6 +156,39 @@ def culling_torture_scene():
     return vc.make_spheres(rows)
 
 
+def random_large_scene(n, seed):
+    """n spheres with log-uniform radii from 5e-4 to 2 (some below the culling margin's r_min),
+    a few huge ones, all materials, in a 60-unit box seen from outside: many hierarchy chunks,
+    tables far beyond LDS, several hits per path."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        c = tuple(float(v) for v in rng.uniform(-30, 30, 3))
+        r = float(np.exp(rng.uniform(np.log(5e-4), np.log(2.0))))
+        if i % 997 == 0:
+            r = float(rng.uniform(5, 15))
+        rows.append((c, r, tuple(rng.uniform(0, 1, 3)), 1 + i % 3, float(rng.uniform(0, 1.6))))
+    return vc.make_spheres(rows)
+
+
+@pytest.mark.parametrize("n", [3000, 9000])
+def test_large_random_scene_all_variants(oracle, n):
+    sc = random_large_scene(n, seed=n)
+    w, h, spp, depth = 40, 24, 2, 8
+    cfg = dict(lookfrom=(-80, 10, 5), lookat=(0, 0, 0), vfov=50)
+    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
+    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE):
+        desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
+                             device=0, kernel_variant=variant, **cfg)
+        with vc.Renderer(desc, sc) as r:
+            r.draw_next_frame()
+            got, st = r.read_framebuffer(), r.stats()
+        assert st["kernel_variant"] == variant and st["nspheres"] == n
+        assert_bitwise(got, want, f"random {n} v{variant}")
+        assert st["segments"] == segs
+
+
 @pytest.mark.parametrize("w,h,spp,depth,chunk", [(64, 40, 8, 12, 0), (33, 21, 5, 50, 5)])
 def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
     sc = culling_torture_scene()

@@ -132,14 +132,36 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
         for (float v : {s[i].center[0], s[i].center[1], s[i].center[2], s[i].radius})
             if (!(std::fabs(v) <= 0x1p30f)) return false;
 
-    // Very large spheres (the ground) would inflate any group they join: group them apart.
+    // Very large spheres (the ground) would inflate any group they join: a sphere is big when
+    // its radius exceeds both 8x the median and 5% of the extent of all centres; at most the
+    // 64 largest go to the big list (tested for every ray), the rest stay in the hierarchy.
     std::vector<float> radii(count);
     for (int32_t i = 0; i < count; i++) radii[i] = std::fabs(s[i].radius);
     std::vector<float> sorted = radii;
     std::nth_element(sorted.begin(), sorted.begin() + count / 2, sorted.end());
-    const float huge = 8.0f * sorted[count / 2];
+    double lo[3], hi[3];
+    for (int a = 0; a < 3; a++) {
+        lo[a] = std::numeric_limits<double>::infinity();
+        hi[a] = -lo[a];
+    }
+    for (int32_t i = 0; i < count; i++)
+        for (int a = 0; a < 3; a++) {
+            lo[a] = std::min(lo[a], static_cast<double>(s[i].center[a]));
+            hi[a] = std::max(hi[a], static_cast<double>(s[i].center[a]));
+        }
+    const double extent = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) +
+                                    (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                    (hi[2] - lo[2]) * (hi[2] - lo[2]));
+    const double huge = std::max(8.0 * sorted[count / 2], 0.05 * extent);
     std::vector<int32_t> normal, big;
     for (int32_t i = 0; i < count; i++) (radii[i] > huge ? big : normal).push_back(i);
+    if (big.size() > 64) {  // keep the 64 largest (ties by index), return the rest
+        std::stable_sort(big.begin(), big.end(),
+                         [&](int32_t x, int32_t y) { return radii[x] > radii[y]; });
+        normal.insert(normal.end(), big.begin() + 64, big.end());
+        big.resize(64);
+        std::sort(big.begin(), big.end());
+    }
     // Big spheres go to a short list the kernels test for every ray (they are hit by most);
     // the rest form the hierarchy: groups of 4, nodes of 8 groups, chunks of 64 groups.
     std::vector<Group> bigg, groups;
