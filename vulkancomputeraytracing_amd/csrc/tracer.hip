@@ -452,14 +452,15 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
     const int ncg = p.ncgroups;
     for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
         exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
-    groups_tested += (uint64_t)p.nbig;
+    // per-segment pass counters, wave-uniform: kept in SGPRs, folded into the 64-bit totals once
+    uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
     uint32_t tops = 0;
     for (int base = 0; base < ncg; base += 64) {
         // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
         if ((base & 127) == 0) {
             const BoundPair tp = load_bound_pair(top + 3 * (base >> 7));
             tops = ~push_bound_pair(0u, r, tp.b0, tp.b1, tp.b2) & 3u;
-            bounds_tested += 2;
+            n_bounds += 2;
         }
         const bool in_chunk = ((tops >> ((base >> 6) & 1)) & 1u) != 0;
         if (__ballot(in_chunk) == 0) continue;
@@ -475,11 +476,11 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             cur = nxt;
         }
         uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
-        bounds_tested += (uint64_t)nn;
+        n_bounds += (uint32_t)nn;
         // level 2, per lane: the groups of this lane's nodes
         uint64_t need = 0;
         while (__ballot(nodes != 0)) {
-            bounds_tested += 8;  // one wave pass = 8 bound tests
+            n_bounds += 8;  // one wave pass = 8 bound tests
             if (nodes) {
                 const int j = __builtin_ctz(nodes);
                 nodes &= nodes - 1;
@@ -496,7 +497,7 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
         if constexpr (kStats) lane_cnt += (uint32_t)__popcll(need);
         // the exact test, per lane on its own groups
         while (__ballot(need != 0)) {
-            ++groups_tested;
+            ++n_groups;
             uint32_t cand = 0;  // stats: candidate roots this lane evaluates in this pass
             if (need) {
                 const int k = __builtin_ctzll(need);
@@ -530,6 +531,8 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             }
         }
     }
+    bounds_tested += __builtin_amdgcn_readfirstlane(n_bounds);
+    groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
 }
 
 // Local element q = 64 * lt + slot of this rank -> pixel (x, y) and its framebuffer index.
