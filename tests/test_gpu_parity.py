@@ -131,7 +131,12 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
     assert st["kernel_variant"] == vc.KERNEL_CULL_LANE
     assert_bitwise(got, want, f"{scene} lane tables={tables}")
     assert st["segments"] == segs
-    assert (st["lds_bytes"] > 0) == (tables == "lds")
+    if tables == "global":
+        assert st["lds_bytes"] == 0
+    elif scene == "final":  # 13 KB of tables: 256-thread workgroups, one copy each
+        assert 0 < st["lds_bytes"] <= 32768 and st["block_threads"] == 256
+    elif st["lds_bytes"] > 0:  # 108 KB: one copy per 1024-thread workgroup
+        assert st["lds_bytes"] > 32768 and st["block_threads"] == 1024
 
 
 def culling_torture_scene():

@@ -20,6 +20,7 @@ for f in ("final", "stress"):
     for lab in os.environ["LABS"].split():
         st = json.load(open(f"gpurun_out/cull_{f}_{lab}.json"))[-1]
         print(f, lab, "Msps %.0f" % st["msamples_per_s"], "kernel_ms %.2f" % st["kernel_ms"],
-              "segs", st["segments"], "groups", st["group_tests"], "bounds", st["bound_tests"])
+              "segs", st["segments"], "groups", st["group_tests"], "bounds", st["bound_tests"],
+              "lds", st["lds_bytes"], "block", st["block_threads"], "grid", st["grid_blocks"])
 PY
 echo all_done

@@ -48,7 +48,8 @@ struct RendererState {
                   k_resolve = nullptr, k_encode = nullptr, k_trace_cull = nullptr,
                   k_trace_cull_stats = nullptr, k_trace_cull_lane_lds = nullptr,
                   k_trace_cull_lane_lds_stats = nullptr, k_trace_cull_lane = nullptr,
-                  k_trace_cull_lane_stats = nullptr;
+                  k_trace_cull_lane_stats = nullptr, k_trace_cull_lane_lds_wide = nullptr,
+                  k_trace_cull_lane_lds_wide_stats = nullptr;
     int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
     bool debug_stats = false;
@@ -188,6 +189,10 @@ VkResult bind_kernels() {
                                   "vcrt_trace_cull_lane_lds_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane, m, "vcrt_trace_cull_lane"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_stats, m, "vcrt_trace_cull_lane_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide, m,
+                                  "vcrt_trace_cull_lane_lds_wide"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide_stats, m,
+                                  "vcrt_trace_cull_lane_lds_wide_stats"));
     return VK_SUCCESS;
 }
 
@@ -527,11 +532,12 @@ vcrt_result vcrt_draw_next_frame(void) {
         }
         // scan table: (groups + 1 padding group) x 64 B
         const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
-        // per-lane culled scan: tables in LDS when they fit in 32 KB (5+ workgroups per CU)
+        // per-lane culled scan: tables in LDS. Up to 32 KB with 256-thread workgroups (5 per
+        // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
+        // copy for 16 waves); beyond that from global memory.
         const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 3 + g.ncgroups * 5));
-        const bool lane_lds = tab_lds <= g.max_lds &&
-                              (g.cull_lane_tables == 1 ||
-                               (g.cull_lane_tables == 0 && tab_lds <= 32768u));
+        const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
+        const bool lane_wide = lane_lds && tab_lds > 32768u;
         int variant = g.desc.kernel_variant;
         // Measured on MI355X: of the linear scans the scalar-cache variant (sphere data in
         // SGPRs, no LDS traffic) beats LDS staging by 15% (485 spheres) and 18% (4100); the
@@ -554,6 +560,10 @@ vcrt_result vcrt_draw_next_frame(void) {
         } else if (variant == VCRT_KERNEL_CULL) {
             f = g.k_trace_cull;
             fs = g.k_trace_cull_stats;
+        } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
+            f = g.k_trace_cull_lane_lds_wide;
+            fs = g.k_trace_cull_lane_lds_wide_stats;
+            lds = tab_lds;
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_lds) {
             f = g.k_trace_cull_lane_lds;
             fs = g.k_trace_cull_lane_lds_stats;
@@ -563,7 +573,7 @@ vcrt_result vcrt_draw_next_frame(void) {
             fs = g.k_trace_cull_lane_stats;
         }
         if (g.debug_stats) f = fs;
-        const uint32_t block = 256;
+        const uint32_t block = (variant == VCRT_KERNEL_CULL_LANE && lane_wide) ? 1024 : 256;
         int per_cu = g.desc.blocks_per_cu;
         if (per_cu <= 0) {
             per_cu = 0;

@@ -827,6 +827,19 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats
     trace_impl<false, true, 2>(p, lds_tab);
 }
 
+// The same with 1024-thread workgroups: one table copy serves 16 waves, so tables of up to
+// 160 KB (the whole LDS of a CU; 4100 spheres take 108 KB) still live in LDS.
+extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_lane_lds_wide(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 2>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_lane_lds_wide_stats(
+    TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, true, 2>(p, lds_tab);
+}
+
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane(TraceParams p) {
     trace_impl<false, false, 3>(p, nullptr);
 }
