@@ -8,7 +8,7 @@ tail -3 gpurun_out/pytest_gpu.log
 run() {  # label variant extra-args...
   local lab=$1 v=$2; shift 2
   timeout -k 10 120 python tools/render_once.py --spp 256 --frames 2 --variant $v "$@" > gpurun_out/cull_final_$lab.json || return 1
-  timeout -k 10 120 python tools/render_once.py --spp 16 --depth 50 --scene stress4096 --frames 2 --variant $v "$@" > gpurun_out/cull_stress_$lab.json || return 1
+  timeout -k 10 120 python tools/render_once.py --width 3840 --height 2160 --spp 32 --depth 50 --scene stress4096 --frames 2 --variant $v "$@" > gpurun_out/cull_stress_$lab.json || return 1
 }
 run smem 2 && run cull 3 && run lane 4 || exit 1
 VCRT_CULL_LANE_TABLES=global run lane_global 4 || exit 1
