@@ -86,8 +86,8 @@ typedef struct vcrt_render_desc {
     int32_t max_depth;         /* MAX_RECURSION_LEVEL, >= 0 */
     vcrt_camera camera;
     int32_t device;        /* HIP device ordinal; -1 = current device */
-    int32_t rank;          /* this process's shard of the frame: the 8x8 tiles t (row-major
-                              tile index) with t % world_size == rank */
+    int32_t rank;          /* this process's shard of the frame: the 8x8 tiles (tx, ty) with
+                              (tx + ty) % world_size == rank, numbered row-major */
     int32_t world_size;    /* number of shards (GPUs) */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */

@@ -58,8 +58,8 @@ def test_gloo_gather_reassembles_bitwise(tmp_path, world):
 
 def test_tile_interleave_balances_the_final_scene_load():
     # Per-pixel segment counts of the bench frame (1920x1080, final scene, depth 10) from a
-    # 1-spp oracle pass, summed per rank: round-robin 8x8 tiles give each of 2/4/8 ranks the mean
-    # load within 1%; contiguous row bands (sky on top, ground below) would not.
+    # 1-spp oracle pass, summed per rank: diagonally interleaved 8x8 tiles give each of 2/4/8
+    # ranks the mean load within 1%; contiguous row bands (sky on top, ground below) would not.
     from tests import oracle_py
     o = oracle_py.load()
     w, h = 1920, 1080
@@ -69,8 +69,8 @@ def test_tile_interleave_balances_the_final_scene_load():
     per_row = np.array([o.render(cfg, scene, rows=range(y, y + 1))[1] for y in range(h)],
                        dtype=np.float64)
     for world in (2, 4, 8):
-        # a tile's cost ~ its rows' cost share over its 8 columns; with t % world and 240 tile
-        # columns (divisible by 8) every rank gets every tile row, 1/world of its columns
+        # a tile's cost ~ its rows' cost share over its 8 columns; with (tx + ty) % world every
+        # rank gets 1/world of every tile row (and, shifted per row, of every column)
         m = tile_pixel_map(w, h, world)[..., 0]
         loads = [(per_row[:, None] / w * (m == r)).sum() for r in range(world)]
         assert max(loads) / np.mean(loads) < 1.01, loads

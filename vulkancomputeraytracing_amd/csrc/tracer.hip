@@ -544,8 +544,8 @@ struct Pixel {
 __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, uint32_t tiles_x,
                                           uint32_t world, uint32_t rank) {
     const uint32_t lt = q >> 6, slot = q & 63u;
-    const uint32_t t = lt * world + rank;
-    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+    uint32_t tx, ty;
+    tile_of(lt, rank, world, tiles_x, &tx, &ty);
     Pixel px;
     px.x = 8u * tx + (slot & 7u);
     px.y = 8u * ty + (slot >> 3);
@@ -613,9 +613,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                 // block b = (local tile lt, chunk): wave-uniform tile origin and sample range
                 blk_lt = b / nchunks;
                 blk_chunk = b - blk_lt * nchunks;
-                const uint32_t t = blk_lt * (uint32_t)p.world + (uint32_t)p.rank;
-                blk_ty = t / p.tiles_x;
-                blk_tx = t - blk_ty * p.tiles_x;
+                tile_of(blk_lt, (uint32_t)p.rank, (uint32_t)p.world, p.tiles_x, &blk_tx, &blk_ty);
                 blk_next = 0u;
             }
             const uint32_t avail = 64u - blk_next;
@@ -886,8 +884,8 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_assemble(AssembleParams p
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += gridDim.x * blockDim.x) {
         const uint32_t y = i / W, x = i - y * W;
-        const uint32_t t = (y >> 3) * p.tiles_x + (x >> 3);
-        const uint32_t r = t % (uint32_t)p.world, lt = t / (uint32_t)p.world;
+        uint32_t r, lt;
+        owner_of(x >> 3, y >> 3, (uint32_t)p.world, p.tiles_x, &r, &lt);
         const uint32_t slot = ((y & 7u) << 3) | (x & 7u);
         p.frame[i] = p.gathered[((size_t)r * p.tiles_per_rank + lt) * 64u + slot];
     }

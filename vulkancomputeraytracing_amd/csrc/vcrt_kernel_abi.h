@@ -13,8 +13,9 @@
 
 namespace vcrt {
 
-// The frame is cut into 8x8 pixel tiles, tile t = ty * tiles_x + tx. Rank r of world owns the
-// tiles t with t % world == r (local tile lt = t / world). Work items are (local tile, sample
+// The frame is cut into 8x8 pixel tiles (tx, ty). Rank r of world owns the tiles with
+// (tx + ty) % world == r, numbered row-major as local tiles lt (vcrt_math.h tile_of /
+// owner_of). Work items are (local tile, sample
 // chunk, slot): 64 consecutive items are one tile at one chunk of samples, one lane per pixel.
 // Rank-local framebuffer: world == 1 -> the frame itself, row-major [H][W]; world > 1 -> packed
 // tiles [local_tiles][64] (slot = 8 * (y % 8) + x % 8), re-interleaved by vcrt_assemble.

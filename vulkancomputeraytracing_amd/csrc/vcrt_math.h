@@ -48,6 +48,47 @@ VCRT_HD f3 reflect(f3 i, f3 n) { return sub(i, scale(2.0f * dot(n, i), n)); }
 VCRT_HD float radians(float deg) { return deg * 0.017453292519943295f; }
 
 // ---------------------------------------------------------------------------------------
+// Frame sharding (DESIGN.md "Multi-GPU"): the 8x8 tile (tx, ty) belongs to rank
+// (tx + ty) % world, and a rank's tiles are numbered in row-major order (local tile lt).
+// Consecutive ranks get consecutive columns of a row, shifted by one per row, so no rank owns a
+// whole column of tiles. Every `world` consecutive rows hold exactly tiles_x tiles of each rank.
+
+// Tiles of row ty owned by rank r: the columns tx = s, s + world, ... with s = (r - ty) mod world.
+VCRT_HD uint32_t tiles_in_row(uint32_t s, uint32_t tiles_x, uint32_t world) {
+    return s < tiles_x ? (tiles_x - 1u - s) / world + 1u : 0u;
+}
+
+// Local tile lt of rank r -> (tx, ty).
+VCRT_HD void tile_of(uint32_t lt, uint32_t r, uint32_t world, uint32_t tiles_x, uint32_t* tx,
+                     uint32_t* ty) {
+    const uint32_t period = lt / tiles_x;
+    uint32_t rem = lt - period * tiles_x, row = period * world, s = r;  // row % world == 0
+    for (;;) {
+        const uint32_t c = tiles_in_row(s, tiles_x, world);
+        if (rem < c) break;
+        rem -= c;
+        ++row;
+        s = s == 0u ? world - 1u : s - 1u;
+    }
+    *tx = s + world * rem;
+    *ty = row;
+}
+
+// Tile (tx, ty) -> its rank and local tile index.
+VCRT_HD void owner_of(uint32_t tx, uint32_t ty, uint32_t world, uint32_t tiles_x, uint32_t* r,
+                      uint32_t* lt) {
+    const uint32_t rank = (tx + ty) % world;
+    const uint32_t j = ty % world;
+    uint32_t n = (ty / world) * tiles_x, s = rank;
+    for (uint32_t k = 0; k < j; ++k) {  // rows ty - j .. ty - 1 of this period
+        n += tiles_in_row(s, tiles_x, world);
+        s = s == 0u ? world - 1u : s - 1u;
+    }
+    *r = rank;
+    *lt = n + tx / world;
+}
+
+// ---------------------------------------------------------------------------------------
 // canonical sin: fp32 argument widened to double, reduced to [-pi/4, pi/4] (Cody-Waite for
 // |x| < 2^20, exact 96-bit integer reduction by 2/pi above), fdlibm kernels, one rounding.
 // Equals the correctly rounded sinf except in astronomically rare double-rounding ties

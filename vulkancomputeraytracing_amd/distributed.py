@@ -1,8 +1,9 @@
-"""Multi-GPU frame sharding: round-robin 8x8 tiles per rank + one framebuffer gather.
+"""Multi-GPU frame sharding: diagonally interleaved 8x8 tiles per rank + one framebuffer gather.
 
-One process per GPU. The frame is cut into 8x8 tiles (row-major tile index t); rank r renders
-the tiles with t % world == r, so every work item stays a coherent 8x8 tile and every rank gets
-the same number of tiles spread over the whole frame (sky and ground alike: SURVEY.md 8(e)).
+One process per GPU. The frame is cut into 8x8 tiles (tx, ty); rank r renders the tiles with
+(tx + ty) % world == r, so every work item stays a coherent 8x8 tile and every rank gets the
+same number of tiles (to one per row) spread over every row and column of the frame (sky and
+ground, left and right alike: SURVEY.md 8(e)).
 The packed rank framebuffers [tiles_per_rank][64] are all-gathered over RCCL
 (``torch.distributed`` backend "nccl") and rank 0 re-interleaves them with the vcrt_assemble
 HIP kernel. The reference is single-GPU (Environment.cpp:157-165; "TODO: Cross-GPU sharing",
@@ -14,8 +15,8 @@ from .renderer import tile_pixel_map, tiles_for_rank  # noqa: F401  (re-exported
 
 
 def tiles_per_rank(width: int, height: int, world: int) -> int:
-    """Tiles of the largest rank (rank 0): the padded per-rank slab of the gather."""
-    return len(tiles_for_rank(width, height, world, 0))
+    """Tiles of the largest rank: the padded per-rank slab of the gather."""
+    return max(len(tiles_for_rank(width, height, world, r)) for r in range(world))
 
 
 def gather_tiles(local, tiles_pad: int, group=None):

@@ -29,7 +29,7 @@ class RenderDesc:
     vfov: float = 20.0
     device: int = -1
     rank: int = 0
-    world_size: int = 1             # shards: rank owns the 8x8 tiles t with t % world == rank
+    world_size: int = 1             # shards: rank owns the 8x8 tiles with (tx + ty) % world == rank
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
     accumulate_chunk: int = 0       # 0 = 16; >= spp: the reference's sequential order
@@ -76,9 +76,11 @@ def effective_chunk(spp: int, accumulate_chunk: int = 0, pixels: int | None = No
 
 
 def tiles_for_rank(width: int, height: int, world: int, rank: int) -> list[int]:
-    """Row-major 8x8 tile indices rank `rank` renders: t % world == rank."""
-    ntiles = ((width + 7) // 8) * ((height + 7) // 8)
-    return list(range(rank, ntiles, world))
+    """Row-major 8x8 tile indices (ty * tiles_x + tx) rank `rank` renders, in its local order:
+    the tiles with (tx + ty) % world == rank (csrc/vcrt_math.h tile_of)."""
+    tx_n, ty_n = (width + 7) // 8, (height + 7) // 8
+    return [ty * tx_n + tx for ty in range(ty_n) for tx in range(tx_n)
+            if (tx + ty) % world == rank]
 
 
 def tile_slots(width: int, height: int, world: int = 1, rank: int = 0) -> int:
@@ -88,10 +90,17 @@ def tile_slots(width: int, height: int, world: int = 1, rank: int = 0) -> int:
 
 def tile_pixel_map(width: int, height: int, world: int) -> np.ndarray:
     """For every frame pixel [y, x]: (rank, element index in that rank's packed tile buffer).
-    The host statement of the index map the vcrt_assemble kernel applies."""
+    The host statement of the index map the vcrt_assemble kernel applies (owner_of)."""
+    tx_n, ty_n = (width + 7) // 8, (height + 7) // 8
+    rank_of = np.zeros((ty_n, tx_n), np.int64)
+    local_of = np.zeros((ty_n, tx_n), np.int64)
+    for r in range(world):
+        for lt, t in enumerate(tiles_for_rank(width, height, world, r)):
+            rank_of[t // tx_n, t % tx_n] = r
+            local_of[t // tx_n, t % tx_n] = lt
     y, x = np.mgrid[0:height, 0:width]
-    t = (y // 8) * ((width + 7) // 8) + x // 8
-    return np.stack([t % world, (t // world) * 64 + (y % 8) * 8 + x % 8], axis=-1)
+    return np.stack([rank_of[y // 8, x // 8],
+                     local_of[y // 8, x // 8] * 64 + (y % 8) * 8 + x % 8], axis=-1)
 
 
 # ---- reference-named lifecycle (VkResult codes, no exceptions) ----------------------------
