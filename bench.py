@@ -2,9 +2,9 @@
 1920x1080, 1024 spp, max depth 10 (BASELINE.json metric, configs[3]) on N MI355X GPUs.
 
 One step = one DrawNextFrame of the whole frame: on every rank the gfx950 tracer renders the
-rank's 8x8 tiles (tile t belongs to rank t % N), then (N > 1) the packed rank framebuffers are
-all-gathered over RCCL and rank 0 re-interleaves the frame. The frame is fixed as N grows
-(strong scaling).
+rank's 8x8 tiles (tile (tx, ty) belongs to rank (tx + ty) % N), then (N > 1) the packed rank
+framebuffers are all-gathered over RCCL and rank 0 re-interleaves the frame. The frame is fixed
+as N grows (strong scaling).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
@@ -225,7 +225,7 @@ def main():
                                    f"{args.spp}spp_d{args.depth}",
                        "scene": args.scene, "spheres": nspheres, "width": args.width,
                        "height": args.height, "spp": args.spp, "max_depth": args.depth,
-                       "parallelism": f"tiles8x8-roundrobin-x{world}",
+                       "parallelism": f"tiles8x8-diagonal-x{world}",
                        "accumulate_chunk": st["accumulate_chunk"],
                        "kernel_variant": st["kernel_variant"],
                        "grid_blocks": st["grid_blocks"]},
