@@ -9,18 +9,22 @@
 //   shaders/include/textures.glsl:19-71  lambertian / metal / glass scatter
 //
 // MI355X design:
-//   * Work items are (8x8 pixel tile, chunk of K samples): one lane per pixel, the chunk's
-//     samples in order. A lane whose path ends starts its next sample at once (path
-//     regeneration); a lane whose chunk is done takes the next item from a wave-aggregated
-//     atomic counter. Chunk sums go to a [chunk][pixel] scratch slab in HBM and vcrt_resolve
-//     adds them in chunk order (K >= spp: no slab, the reference's sequential sum).
-//   * Ray state lives in VGPRs. The sphere list is stored as pair-SoA groups of four
-//     (cx0 cx1 cy0 cy1 | cz0 cz1 r0^2 r1^2 | ...) and tested two spheres per packed-fp32
-//     instruction (v_pk_add_f32 / v_pk_mul_f32: 2 lane-ops per issue, the only way gfx950
-//     reaches its fp32 peak). Staged once per workgroup in LDS (kLds) or read with
-//     wave-uniform scalar loads (!kLds); all lanes test the same spheres at the same time.
-//   * Only fp32 add/sub/mul plus correctly rounded div/sqrt, no contraction: results are
-//     bit-identical to the CPU oracle for the same accumulation order. No MFMA.
+//   * Work items are (8x8 pixel tile, chunk of K samples, slot): one lane per pixel, the
+//     chunk's samples in order. A wave takes a whole block (one tile at one chunk = 64 items)
+//     with one atomic and hands its slots to lanes as they free up; a lane whose path ends
+//     starts its next sample at once (path regeneration). Chunk sums go to a [chunk][pixel]
+//     slab in HBM and vcrt_resolve adds them in chunk order (K >= spp: no slab, the
+//     reference's sequential sum).
+//   * Ray state lives in VGPRs. Sphere tests run two spheres per packed-fp32 instruction
+//     (v_pk_add_f32 / v_pk_mul_f32 on pair-SoA groups of four: 2 lane-ops per issue, the only
+//     way gfx950 reaches its fp32 peak).
+//   * The sphere-list scan is either the reference's linear scan (wave-uniform groups through
+//     the scalar cache or LDS) or an exact culled scan over a spatial hierarchy (groups of 4,
+//     nodes of 8 groups, chunks of 64 groups), wave-uniform or per lane on an LDS copy of the
+//     tables; see "Culled scan" below for why it returns the same sphere and t.
+//   * Only fp32 add/sub/mul plus correctly rounded div/sqrt, no contraction, in everything
+//     that reaches the image: results are bit-identical to the CPU oracle for the same
+//     accumulation order. No MFMA.
 #include <hip/hip_runtime.h>
 
 #include "vcrt_kernel_abi.h"
@@ -195,8 +199,10 @@ __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
 }
 
 // A member whose origin lies outside or on it (cc >= 0) while the ray points away from its
-// centre (hb >= 0) can never be accepted: disc_f <= RN(hb^2), RN(sqrt(RN(hb^2))) = hb, so
-// RN(-hb + sq) <= 0 and both roots are <= 0 < min_t. (Padding members never hit: their
+// centre (hb >= 0) can never be accepted: disc_f <= RN(hb^2) and RN(sqrt(RN(hb^2))) = hb
+// (binary fp, no underflow), so RN(-hb + sq) <= 0 and both roots are <= 0 < min_t. If hb^2
+// underflows (hb < 2^-63), -hb + sq is below 2^-100 and root2 < 2^-80 < min_t all the same.
+// A -0 hb only adds candidates; cc is never -0. (Padding members never hit: their
 // r^2 = -3e38 makes disc negative or -inf.)
 __device__ __forceinline__ bool may_hit(float hb, float cc, float disc) {
     return !(disc < 0.0f) && (hb < 0.0f || cc < 0.0f);
