@@ -201,8 +201,8 @@ __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
 // A member whose origin lies outside or on it (cc >= 0) while the ray points away from its
 // centre (hb >= 0) can never be accepted: disc_f <= RN(hb^2) and RN(sqrt(RN(hb^2))) = hb
 // (binary fp, no underflow), so RN(-hb + sq) <= 0 and both roots are <= 0 < min_t. If hb^2
-// underflows (hb < 2^-63), RN(hb^2) is off by at most 2^-150, so -hb + sq < 2^-75 and, with
-// a >= 2^-20, root2 < 2^-55 < min_t all the same.
+// underflows (hb < 2^-63), RN(hb^2) is off by at most 2^-149, so -hb + sq < 2^-74 and, with
+// a >= 2^-20, root2 < 2^-54 < min_t all the same.
 // A -0 hb only adds candidates; cc is never -0. (Padding members never hit: their
 // r^2 = -3e38 makes disc negative or -inf.)
 __device__ __forceinline__ bool may_hit(float hb, float cc, float disc) {
