@@ -78,6 +78,7 @@ typedef struct vcrt_camera { /* globals.glsl:21-24 */
 #define VCRT_KERNEL_SMEM 2
 #define VCRT_KERNEL_CULL 3
 #define VCRT_KERNEL_CULL_LANE 4 /* CULL with per-lane group tests (LDS or global tables) */
+#define VCRT_KERNEL_CULL_FLAT 5 /* CULL_LANE with the exact tests dealt out over the wave */
 
 typedef struct vcrt_render_desc {
     uint32_t struct_size;      /* sizeof(vcrt_render_desc) */

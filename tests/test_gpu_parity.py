@@ -54,8 +54,9 @@ CASES = [
 ]
 
 
-VARIANTS = [vc.KERNEL_LDS, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE]
-CULLED = (vc.KERNEL_CULL, vc.KERNEL_CULL_LANE)
+VARIANTS = [vc.KERNEL_LDS, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE,
+            vc.KERNEL_CULL_FLAT]
+CULLED = (vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT)
 
 
 def expected_variant(variant, nspheres):
@@ -112,7 +113,8 @@ def test_golden_oracle_images():
 def test_stress_scene_small(oracle):
     w, h, spp, depth = 48, 27, 2, 10
     want, segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("stress4096"))
-    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE):
+    for variant in (vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE,
+                    vc.KERNEL_CULL_FLAT):
         got, st = gpu_render("stress4096", w, h, spp, depth, variant)
         assert_bitwise(got, want, f"stress v{variant}")
         assert st["segments"] == segs and st["nspheres"] == 4100
@@ -183,13 +185,15 @@ def test_large_random_scene_all_variants(oracle, n):
     cfg = dict(lookfrom=(-80, 10, 5), lookat=(0, 0, 0), vfov=50)
     k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
-    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE):
+    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, kernel_variant=variant, **cfg)
         with vc.Renderer(desc, sc) as r:
             r.draw_next_frame()
             got, st = r.read_framebuffer(), r.stats()
-        assert st["kernel_variant"] == variant and st["nspheres"] == n
+        # CULL_FLAT needs its tables in LDS: these scenes fall back to CULL_LANE
+        want_v = vc.KERNEL_CULL_LANE if variant == vc.KERNEL_CULL_FLAT else variant
+        assert st["kernel_variant"] == want_v and st["nspheres"] == n
         assert_bitwise(got, want, f"random {n} v{variant}")
         assert st["segments"] == segs
 
@@ -201,7 +205,7 @@ def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
     cfg = dict(lookfrom=(6, 2.5, 5), lookat=(0, 0.6, 0), vfov=45)
     k = vc.renderer.effective_chunk(spp, chunk, pixels=vc.tile_slots(w, h))
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
-    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE):
+    for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, kernel_variant=variant, accumulate_chunk=chunk, **cfg)
         with vc.Renderer(desc, sc) as r:
@@ -333,7 +337,8 @@ def test_reference_named_lifecycle():
     vc.SetRenderScene(None)
 
 
-@pytest.mark.parametrize("variant", [vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL_LANE])
+@pytest.mark.parametrize("variant", [vc.KERNEL_AUTO, vc.KERNEL_SMEM, vc.KERNEL_CULL_LANE,
+                                     vc.KERNEL_CULL_FLAT])
 def test_full_size_rows_subset_rms(oracle, variant):
     # BASELINE config 3 geometry (1920x1080, depth 10) at 16 spp; oracle renders every 90th row.
     w, h, spp, depth = 1920, 1080, 16, 10

@@ -10,9 +10,9 @@ run() {  # label variant extra-args...
   timeout -k 10 120 python tools/render_once.py --spp 256 --frames 2 --variant $v "$@" > gpurun_out/cull_final_$lab.json || return 1
   timeout -k 10 120 python tools/render_once.py --width 3840 --height 2160 --spp 32 --depth 50 --scene stress4096 --frames 2 --variant $v "$@" > gpurun_out/cull_stress_$lab.json || return 1
 }
-run smem 2 && run cull 3 && run lane 4 || exit 1
+run smem 2 && run cull 3 && run lane 4 && run flat 5 || exit 1
 VCRT_CULL_LANE_TABLES=global run lane_global 4 || exit 1
-labs="smem cull lane lane_global"
+labs="smem cull lane flat lane_global"
 for lv in $VARIANTS; do run "${lv%%=*}" ${VARIANT_ID:-3} --code-object "${lv#*=}" || exit 1; labs="$labs ${lv%%=*}"; done
 LABS="$labs" python - <<'PY'
 import json, os

@@ -7,7 +7,7 @@ host API (Renderer Begin/Draw/End, Shader loading, SceneGenerator) over that ABI
 """
 from . import _native
 from ._native import (VK_SUCCESS, VK_ERROR_INITIALIZATION_FAILED, VcrtError, KERNEL_AUTO,
-                      KERNEL_LDS, KERNEL_SMEM, KERNEL_CULL, KERNEL_CULL_LANE,
+                      KERNEL_LDS, KERNEL_SMEM, KERNEL_CULL, KERNEL_CULL_LANE, KERNEL_CULL_FLAT,
                       TEXTURE_GLASS, TEXTURE_LAMBERTIAN, TEXTURE_METAL)
 from .renderer import (BeginRenderingOperation, DrawNextFrame, EndRenderingOperation, Renderer,
                        RenderDesc, SetRenderDescription, SetRenderScene, render, tile_pixel_map,
@@ -20,5 +20,5 @@ __all__ = [
     "tile_slots", "tile_pixel_map",
     "SPHERE_DTYPE", "builtin_scene", "make_spheres", "scene_generator_text", "VcrtError",
     "VK_SUCCESS", "VK_ERROR_INITIALIZATION_FAILED", "KERNEL_AUTO", "KERNEL_LDS", "KERNEL_SMEM",
-    "KERNEL_CULL", "KERNEL_CULL_LANE", "TEXTURE_GLASS", "TEXTURE_LAMBERTIAN", "TEXTURE_METAL", "_native",
+    "KERNEL_CULL", "KERNEL_CULL_LANE", "KERNEL_CULL_FLAT", "TEXTURE_GLASS", "TEXTURE_LAMBERTIAN", "TEXTURE_METAL", "_native",
 ]

@@ -34,6 +34,7 @@ KERNEL_LDS = 1
 KERNEL_SMEM = 2
 KERNEL_CULL = 3
 KERNEL_CULL_LANE = 4
+KERNEL_CULL_FLAT = 5
 
 SCENE_FINAL = 0
 SCENE_THREE = 1

@@ -49,7 +49,8 @@ struct RendererState {
                   k_trace_cull_stats = nullptr, k_trace_cull_lane_lds = nullptr,
                   k_trace_cull_lane_lds_stats = nullptr, k_trace_cull_lane = nullptr,
                   k_trace_cull_lane_stats = nullptr, k_trace_cull_lane_lds_wide = nullptr,
-                  k_trace_cull_lane_lds_wide_stats = nullptr;
+                  k_trace_cull_lane_lds_wide_stats = nullptr, k_trace_cull_flat = nullptr,
+                  k_trace_cull_flat_stats = nullptr;
     int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
     bool debug_stats = false;
@@ -195,6 +196,8 @@ VkResult bind_kernels() {
                                   "vcrt_trace_cull_lane_lds_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane, m, "vcrt_trace_cull_lane"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_stats, m, "vcrt_trace_cull_lane_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat, m, "vcrt_trace_cull_flat"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_stats, m, "vcrt_trace_cull_flat_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide, m,
                                   "vcrt_trace_cull_lane_lds_wide"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide_stats, m,
@@ -229,7 +232,7 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
     if (d.progressive != 0 && d.progressive != 1) return false;
-    if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL_LANE) return false;
+    if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL_FLAT) return false;
     return true;
 }
 
@@ -558,9 +561,13 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (variant == VCRT_KERNEL_AUTO)
             variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_LANE;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
-        if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE) &&
+        if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE ||
+             variant == VCRT_KERNEL_CULL_FLAT) &&
             g.ncgroups == 0)
             variant = VCRT_KERNEL_SMEM;
+        // the flattened exact phase needs its tables in LDS beside 3.5 KB of scratch per wave
+        constexpr uint32_t kFlatScratch = 4 * vcrt::kWaveScratchBytes;  // 4 waves per block
+        if (variant == VCRT_KERNEL_CULL_FLAT && (!lane_lds || lane_wide)) variant = VCRT_KERNEL_CULL_LANE;
         hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
         uint32_t lds = 0;
         if (variant == VCRT_KERNEL_LDS) {
@@ -570,6 +577,10 @@ vcrt_result vcrt_draw_next_frame(void) {
         } else if (variant == VCRT_KERNEL_CULL) {
             f = g.k_trace_cull;
             fs = g.k_trace_cull_stats;
+        } else if (variant == VCRT_KERNEL_CULL_FLAT) {
+            f = g.k_trace_cull_flat;
+            fs = g.k_trace_cull_flat_stats;
+            lds = tab_lds + kFlatScratch;
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
             f = g.k_trace_cull_lane_lds_wide;
             fs = g.k_trace_cull_lane_lds_wide_stats;

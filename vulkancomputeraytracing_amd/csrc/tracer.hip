@@ -437,13 +437,148 @@ __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
     return __uint_as_float((__float_as_uint(hb) | __float_as_uint(cc)) & ~__float_as_uint(disc));
 }
 
-template <bool kStats>
+// ---- flattened exact phase (variant CULL_FLAT) ----------------------------------------------
+// The per-lane exact loop runs as many passes as the wave's busiest lane needs groups (10 when
+// the mean lane needs 5). Here the wave's (lane, group) pairs are listed in LDS and dealt out
+// 64 per pass, each lane testing another lane's ray (fetched with ds_bpermute); candidate roots
+// are listed as well and resolved 64 at a time; every owner's (t, sphere index) minimum is kept
+// in an LDS 64-bit word updated with ds_min_u64 -- the lexicographic minimum of (t, index) is
+// exactly what `consider` computes, since t > 0 orders like its bit pattern.
+constexpr int kPairCap = 512;   // pairs per chunk and wave (more: per-lane loop instead)
+constexpr int kCandCap = 128;   // candidate roots listed before a resolve round
+
+struct WaveScratch {
+    unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
+    float4 cand[kCandCap];       // hb, disc, a, index | owner << 24
+    uint16_t pair[kPairCap];     // owner << 6 | group within the chunk
+};
+static_assert(sizeof(WaveScratch) == kWaveScratchBytes, "host LDS size");
+
+__device__ __forceinline__ unsigned long long pack_hit(float t, int idx) {
+    return ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)idx;
+}
+
+// Exclusive prefix of a per-lane count c < 128 over the active lanes, and the wave total,
+// from bit-sliced ballots (inactive lanes count as 0).
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const uint64_t m = __ballot((c >> b) & 1u);
+        pre += lanes_below(m) << b;
+        tot += (uint32_t)__popcll(m) << b;
+    }
+    total = tot;
+    return pre;
+}
+
+// Resolve the listed candidate roots, 64 per pass, into the owners' keys.
+__device__ __forceinline__ void resolve_cands(WaveScratch* ws, uint32_t ncand, uint32_t rank,
+                                              uint32_t nact) {
+    for (uint32_t c0 = 0; c0 < ncand; c0 += nact) {
+        const uint32_t j = c0 + rank;
+        if (j < ncand) {
+            const float4 cd = ws->cand[j];
+            const float t = candidate_t(cd.x, cd.y, cd.z);
+            const uint32_t w = __float_as_uint(cd.w);
+            if (t > 0.001f && t < 1e5f)
+                atomicMin(&ws->key[w >> 24], pack_hit(t, (int)(w & 0xFFFFFFu)));
+        }
+    }
+}
+
+// The exact test of this chunk's needed groups, flattened over the wave. Returns false (and
+// does nothing) when the wave needs more than kPairCap pairs in this chunk.
+__device__ __forceinline__ bool exact_flat(WaveScratch* ws, const float4* tg, uint64_t need,
+                                           const f3 o, const f3 d, float a, uint32_t lane,
+                                           uint32_t& n_passes) {
+    // only the wave's live lanes run this (finished lanes are masked off): pairs and
+    // candidates are dealt by rank among the live lanes, nact per pass
+    const uint64_t live = __ballot(1);
+    const uint32_t nact = (uint32_t)__popcll(live), rank = lanes_below(live);
+    const uint32_t cnt = (uint32_t)__popcll(need);
+    uint32_t total;
+    const uint32_t pre = wave_prefix(cnt, total);
+    if (total > (uint32_t)kPairCap) return false;
+    {  // list my pairs
+        uint64_t m = need;
+        uint32_t pos = pre;
+        while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            ws->pair[pos++] = (uint16_t)((lane << 6) | k);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t ncand = 0;  // wave-uniform
+    for (uint32_t i0 = 0; i0 < total; i0 += nact) {
+        ++n_passes;
+        const uint32_t i = i0 + rank;
+        const bool act = i < total;
+        const uint32_t pr = act ? (uint32_t)ws->pair[i] : (lane << 6);
+        const int owner = (int)(pr >> 6);
+        // the owner's ray (ds_bpermute; owners are active lanes)
+        const float qx = __shfl(o.x, owner), qy = __shfl(o.y, owner), qz = __shfl(o.z, owner);
+        const float ex = __shfl(d.x, owner), ey = __shfl(d.y, owner), ez = __shfl(d.z, owner);
+        const float qa = __shfl(a, owner);
+        uint32_t hits = 0;
+        v2f hb01, cc01, d01, hb23, cc23, d23;
+        float4 idf = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (act) {
+            const float4* g = tg + __umul24(pr & 63u, 5u);
+            const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
+            const v2f ox = {qx, qx}, oy = {qy, qy}, oz = {qz, qz};
+            const v2f dx = {ex, ex}, dy = {ey, ey}, dz = {ez, ez}, a2 = {qa, qa};
+            pair_disc_cc(ox, oy, oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+            pair_disc_cc(ox, oy, oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+            hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
+            hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
+            hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
+            hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
+            if (hits) idf = g[4];
+        }
+        // list the candidates (a full list is resolved first)
+        uint32_t ctot;
+        const uint32_t cpre = wave_prefix((uint32_t)__popc(hits), ctot);
+        if (ncand + ctot > (uint32_t)kCandCap) {
+            __builtin_amdgcn_wave_barrier();
+            resolve_cands(ws, ncand, rank, nact);
+            __builtin_amdgcn_wave_barrier();
+            ncand = 0;
+        }
+        const bool direct = ctot > (uint32_t)kCandCap;  // more than the list holds: in place
+        uint32_t pos = ncand + cpre;
+        const uint32_t ownbits = (uint32_t)owner << 24;
+        while (hits) {
+            const int s = __builtin_ctz(hits);
+            hits &= hits - 1;
+            const float hb = s == 0 ? hb01.x : s == 1 ? hb01.y : s == 2 ? hb23.x : hb23.y;
+            const float ds = s == 0 ? d01.x : s == 1 ? d01.y : s == 2 ? d23.x : d23.y;
+            const float ix = s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w;
+            if (direct) {
+                const float t = candidate_t(hb, ds, qa);
+                if (t > 0.001f && t < 1e5f)
+                    atomicMin(&ws->key[owner], pack_hit(t, (int)__float_as_uint(ix)));
+            } else {
+                ws->cand[pos++] =
+                    make_float4(hb, ds, qa, __uint_as_float(__float_as_uint(ix) | ownbits));
+            }
+        }
+        if (!direct) ncand += ctot;
+    }
+    __builtin_amdgcn_wave_barrier();
+    resolve_cands(ws, ncand, rank, nact);
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+template <bool kStats, bool kFlat = false>
 __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const float4* tbound,
                                                  const float4* tgroup, const f3 o, const f3 d,
                                                  float& max_t, int& best,
                                                  uint64_t& groups_tested,
                                                  uint64_t& bounds_tested, uint32_t& lane_cnt,
-                                                 uint32_t& rounds) {
+                                                 uint32_t& rounds, WaveScratch* ws = nullptr) {
     const float a = dot(d, d);
     const float inv = __builtin_amdgcn_rsqf(a);
     CullRay r;
@@ -461,6 +596,8 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
         exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
     // per-segment pass counters, wave-uniform: kept in SGPRs, folded into the 64-bit totals once
     uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
+    const uint32_t lane = threadIdx.x & 63u;
+    if constexpr (kFlat) ws->key[lane] = pack_hit(max_t, best);
     uint32_t tops = 0;
     for (int base = 0; base < ncg; base += 64) {
         // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
@@ -502,6 +639,14 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             }
         }
         if constexpr (kStats) lane_cnt += (uint32_t)__popcll(need);
+        if constexpr (kFlat) {
+            if (exact_flat(ws, tgroup + 5 * base, need, o, d, a, lane, n_groups)) continue;
+            // too many pairs for the list: the per-lane loop, on registers synced with the key
+            __builtin_amdgcn_wave_barrier();
+            const unsigned long long k = ws->key[lane];
+            max_t = __uint_as_float((uint32_t)(k >> 32));
+            best = (int)(uint32_t)k;
+        }
         // the exact test, per lane on its own groups
         while (__ballot(need != 0)) {
             ++n_groups;
@@ -537,6 +682,13 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
                 rounds += cand;
             }
         }
+        if constexpr (kFlat) ws->key[lane] = pack_hit(max_t, best);
+    }
+    if constexpr (kFlat) {
+        __builtin_amdgcn_wave_barrier();
+        const unsigned long long k = ws->key[lane];
+        max_t = __uint_as_float((uint32_t)(k >> 32));
+        best = (int)(uint32_t)k;
     }
     bounds_tested += __builtin_amdgcn_readfirstlane(n_bounds);
     groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
@@ -573,13 +725,16 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     }
     const float4* tbound = p.cbound;
     const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
-    if constexpr (kCull == 2) {
+    WaveScratch* ws = nullptr;
+    if constexpr (kCull == 2 || kCull == 4) {
         const int nb = (p.ncgroups >> 1) * 3, ng = p.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = p.cbound[i];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = tgroup[i];
         __syncthreads();
         tbound = lds_geom;
         tgroup = lds_geom + nb;
+        if constexpr (kCull == 4)
+            ws = reinterpret_cast<WaveScratch*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
     }
     const uint32_t lane = threadIdx.x & 63u;
     const f3 p00 = mk(p.cam[0], p.cam[1], p.cam[2]);
@@ -674,6 +829,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                 if constexpr (kCull == 1)
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
+                else if constexpr (kCull == 4)
+                    scan_culled_lane<kStats, true>(p, tbound, tgroup, o, d, max_t, best,
+                                                   w_groups, w_bounds, lane_cnt, hit_groups, ws);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);
@@ -830,6 +988,18 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds(Trace
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, true, 2>(p, lds_tab);
+}
+
+// Per-lane scan with the exact phase flattened over the wave (exact_flat): LDS tables plus
+// 3.5 KB of scratch per wave.
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void vcrt_trace_cull_flat(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 4>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_stats(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, true, 4>(p, lds_tab);
 }
 
 // The same with 1024-thread workgroups: one table copy serves 16 waves, so tables of up to

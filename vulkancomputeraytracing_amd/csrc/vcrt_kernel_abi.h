@@ -54,6 +54,7 @@ struct TraceParams {
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
 };
 
+constexpr uint32_t kWaveScratchBytes = 3584;  // CULL_FLAT per-wave LDS scratch (tracer.hip)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 constexpr uint32_t kFlagSlab = 4u;          // chunk sums always go to the slab (resolve pass)
