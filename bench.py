@@ -20,10 +20,10 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector, MI355X_MICROARCH.md chip table
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
-FLOPS_PER_BOUND_TEST = 18       # tracer.hip bound_pair_need, per bound: oc 3, |oC|^2 5, h 5,
-                                # X 2, RM 2, RM^2 1
+FLOPS_PER_BOUND_TEST = 26       # tracer.hip box_gap, per box: 6 fma 12, per-axis min/max 6,
+                                # tnear/tfar 4, gap sub + add + fma 4
 KERNEL_NAMES = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull",
-                4: "vcrt_trace_cull_lane"}
+                4: "vcrt_trace_cull_lane", 5: "vcrt_trace_cull_flat"}
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -191,12 +191,12 @@ def main():
         # numerator is what the kernel actually issued -- every lane of each wave-level group
         # test (4 spheres x 23) and bound test (18) -- which is all there is for the linear scan.
         executed = flops
-        if st["kernel_variant"] in (3, 4):
+        if st["kernel_variant"] in (3, 4, 5):
             executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
                         + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
         kernel = KERNEL_NAMES.get(st["kernel_variant"], "?")
         if st["kernel_variant"] == 4 and st["lds_bytes"] > 0:
-            kernel += "_lds"
+            kernel += "_lds_wide" if st["block_threads"] == 1024 else "_lds"
         achieved = executed / (k_ms * 1e-3) / 1e12
         equivalent = flops / (k_ms * 1e-3) / 1e12
         traffic = None
@@ -235,7 +235,7 @@ def main():
                          "kernel": kernel, "kernel_ms": round(k_ms, 3),
                          "numerator": "issued sphere-test and bound-test flops per launch "
                                       "(DESIGN.md 5): wave-level group tests x 64 x 4 x 23 + "
-                                      "bound tests x 64 x 18",
+                                      "bound tests x 64 x 26 (box_gap)",
                          "flops_per_launch": executed,
                          "segments_per_launch": int(seg),
                          "reference_equivalent_flops_per_launch": flops,

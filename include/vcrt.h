@@ -177,19 +177,21 @@ int32_t vcrt_scene_builtin(int32_t scene_id, vcrt_sphere* out, int32_t cap);
 size_t vcrt_scene_generator_text(char* buf, size_t cap);
 
 /* The culled scans' grouped tables for a sphere list (host only, no GPU). The big spheres
- * (radius > 8x the median) form a short list of groups tested for every ray (*big_groups of
- * them, written first to geom/index); the rest form the hierarchy. Tables: groups of four in
- * pair-SoA form (16 floats each), hierarchy group-pair bounds (12 floats per two groups: Cx0
- * Cx1 Cy0 Cy1 Cz0 Cz1 K0 K1 Rk0 Rk1 0 0; a ray rules bound i out when its squared line
- * distance exceeds (K_i |o - C_i|^2 + Rk_i)^2, see csrc/tracer.hip), node-pair bounds (same
- * form; node i covers hierarchy groups 8i..8i+7), top-level bounds (same form; entry i covers
- * hierarchy groups 64i..64i+63, count ceil(G/64) rounded up to even) and member indices (4 per
- * group, -1 = padding). Returns the hierarchy group count G, a multiple of 16 (0 = culling does
- * not apply: < 16 spheres or unbounded scene), and writes the tables when cap_groups >=
- * *big_groups + G (any pointer may be NULL). */
+ * (radius > 8x the median and 5% of the centres' extent) form a short list of groups tested
+ * for every ray (*big_groups of them, written first to geom/index); the rest form the
+ * hierarchy. Tables: groups of four in pair-SoA form (16 floats each), hierarchy group-pair
+ * boxes (16 floats per two groups: lox0 lox1 loy0 loy1 loz0 loz1 hix0 hix1 hiy0 hiy1 hiz0 hiz1
+ * K0 K1 0 0 -- the members' extent rounded outwards and K = 8.1u / r_min of the members; a ray
+ * rules box i out when its line misses the box grown by its margin, see csrc/tracer.hip
+ * box_gap), node-pair boxes (same form; node i covers hierarchy groups 8i..8i+7), top-level
+ * boxes (same form; entry i covers hierarchy groups 64i..64i+63, count ceil(G/64) rounded up to
+ * even), member indices (4 per group, -1 = padding) and margin4 = {max |centre|, r_max^2, max
+ * |box coordinate|, 0} over the hierarchy (rounded up). Returns the hierarchy group count G, a
+ * multiple of 16 (0 = culling does not apply: < 16 spheres or unbounded scene), and writes the
+ * tables when cap_groups >= *big_groups + G (any pointer may be NULL). */
 int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
                          float* node, float* top, int32_t* index, int32_t* big_groups,
-                         int32_t cap_groups);
+                         float* margin4, int32_t cap_groups);
 
 /* Canonical math as used by the kernel (host evaluation), for tests and tools. */
 float vcrt_canonical_sin(float x);

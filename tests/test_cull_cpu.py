@@ -1,10 +1,11 @@
 """CPU checks of the CULL variant's grouped tables (vcrt_cull_tables, csrc/cluster.cpp).
 
 The culled scan is exact only if (1) every sphere sits in exactly one group with the linear
-table's values, and (2) a group whose bound test culls it for a ray holds no sphere whose fp32
-discriminant (hit_sphere, functions.glsl:14-22, as tracer.hip's pair_disc evaluates it) is
->= 0. (2) is checked here by emulating both fp32 evaluations in numpy on random rays and on
-rays built to graze member spheres within 1e-7..1e-4 of their radius.
+table's values, and (2) a group whose box test rules it out for a ray holds no sphere whose
+fp32 discriminant (hit_sphere, functions.glsl:14-22, as tracer.hip's pair_disc evaluates it) is
+>= 0. (2) is checked here by emulating both fp32 evaluations in numpy on random rays (near and
+far origins), on rays built to graze member spheres within 1e-7..1e-4 of their radius, and on
+rays grazing a member where it touches its box.
 """
 import numpy as np
 import pytest
@@ -19,29 +20,60 @@ def fma(x, y, z):
     return (x.astype(np.float64) * y.astype(np.float64) + z.astype(np.float64)).astype(f32)
 
 
+def rn(x):
+    return np.asarray(x, np.float64).astype(f32)
+
+
+def ulp_noise(x, rng, ulps=1):
+    """x perturbed by up to `ulps` ulp (v_rcp_f32 / v_sqrt_f32 are 1 ulp accurate)."""
+    if rng is None:
+        return x
+    k = rng.integers(-ulps, ulps + 1, x.shape)
+    out = x.copy()
+    for step in range(1, ulps + 1):
+        out = np.where(k >= step, np.nextafter(out, f32(np.inf)), out)
+        out = np.where(k <= -step, np.nextafter(out, f32(-np.inf)), out)
+    return out.astype(f32)
+
+
+def box_ray(t, o, d, rng=None):
+    """tracer.hip box_ray in fp32: per axis inv = v_rcp(d'), c = -o inv; c1, c2."""
+    cmax, rmax2, lam = (f32(v) for v in t["margin"][:3])
+    dd = np.where(np.abs(d) < f32(2.0 ** -40), np.copysign(f32(2.0 ** -40), d), d).astype(f32)
+    inv = ulp_noise(rn(1.0 / dd.astype(np.float64)), rng)
+    c = rn(-o.astype(np.float64) * inv)
+    J = rn(f32(2.002) * np.abs(inv).max(1))
+    dot = rn(rn(rn(o[:, 0] * o[:, 0]) + rn(o[:, 1] * o[:, 1])) + rn(o[:, 2] * o[:, 2]))
+    on = rn(ulp_noise(rn(np.sqrt(dot.astype(np.float64))), rng) + cmax)
+    Q = rn(rn(on * on) + rmax2)
+    oinf = np.abs(o).max(1)
+    c1 = rn(J * rn(f32(3.04e-7) * rn(lam + oinf)))
+    c2 = rn(J * Q)
+    return inv, c, c1, c2
+
+
 def group_culled(t, o, d, key="bound", rng=None):
-    """[rays, bounds] bool: the kernel's bound test (tracer.hip bound_pair_need) on the group
-    bounds (key "bound") or the node bounds ("node"). v_rsq_f32's error (~1 ulp) is emulated
-    by a random +-2 ulp perturbation of the exact reciprocal square root."""
+    """[rays, boxes] bool: the kernel's box test (tracer.hip box_gap, fact (3)) on the group
+    boxes (key "bound"), the node boxes ("node") or the chunk boxes ("top"), in fp32 with
+    v_rcp_f32 / v_sqrt_f32's 1-ulp errors emulated by random perturbations (rng)."""
     b = t[key]
     G = 2 * b.shape[0]
     cols = lambda k: np.stack([b[:, k], b[:, k + 1]], 1).reshape(G)  # noqa: E731
-    C = [cols(0), cols(2), cols(4)]
-    K, Rk = cols(6), cols(8)
-    a = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
-    inv = (1.0 / np.sqrt(a.astype(np.float64))).astype(f32)
-    if rng is not None:
-        inv = (inv * (1 + rng.uniform(-2.4e-7, 2.4e-7, inv.shape))).astype(f32)
-    w = (d * inv[:, None]).astype(f32)
-    oc = [(o[:, k, None] - C[k][None, :]).astype(f32) for k in range(3)]
-    ww = [np.broadcast_to(w[:, k, None], oc[0].shape) for k in range(3)]
-    oc2 = fma(oc[2], oc[2], fma(oc[1], oc[1], oc[0] * oc[0]))
-    h = fma(oc[2], ww[2], fma(oc[1], ww[1], oc[0] * ww[0]))
-    X = fma(-h, h, oc2)
-    with np.errstate(invalid="ignore", over="ignore"):
-        RM = fma(np.broadcast_to(K, oc2.shape), oc2, np.broadcast_to(Rk, oc2.shape))
-        T = RM * RM
-        return X > T
+    lo = [cols(0), cols(2), cols(4)]
+    hi = [cols(6), cols(8), cols(10)]
+    K = cols(12)
+    inv, c, c1, c2 = box_ray(t, o, d, rng)
+    tn = tf = None
+    for k in range(3):
+        tl = fma(lo[k][None, :], inv[:, k, None], c[:, k, None])
+        th = fma(hi[k][None, :], inv[:, k, None], c[:, k, None])
+        near, far = np.minimum(tl, th), np.maximum(tl, th)
+        tn = near if tn is None else np.maximum(tn, near)
+        tf = far if tf is None else np.minimum(tf, far)
+    with np.errstate(over="ignore", invalid="ignore"):
+        gap = fma(np.broadcast_to(K[None, :], tn.shape), np.broadcast_to(c2[:, None], tn.shape),
+                  rn(rn(tf - tn) + c1[:, None]))
+    return gap < 0
 
 
 def member_disc(t, o, d):
@@ -78,31 +110,25 @@ def grazing_rays(spheres, n, rng):
     return o, d
 
 
-def bound_of(t, gi):
-    e, bb = gi % 2, t["bound"][gi // 2]
-    return np.array([bb[0 + e], bb[2 + e], bb[4 + e]], np.float64)
-
-
 def tangent_rays(spheres, t, n, rng):
-    """Rays tangent to a group's outermost member on the side facing away from the group
-    centre: they graze the member where it touches the bounding sphere (the tightest case for
-    the bound test)."""
+    """Rays that graze a group's extreme member where it touches a face of the group's box
+    (the tightest case for the box test): touching point c +- r e_a, direction in the face."""
     G = t["geom"].shape[0] - t["nbig"]
     os_, ds_ = [], []
     for gi in rng.integers(0, G, n):
-        C = bound_of(t, gi)
         idx = t["index"][t["nbig"] + gi]
         m = idx[idx >= 0]
         if len(m) == 0:
             continue
         c = spheres["center"][m].astype(np.float64)
         r = np.abs(spheres["radius"][m].astype(np.float64))
-        i = np.argmax(np.linalg.norm(c - C, axis=1) + r)
-        u = c[i] - C
-        u = u / np.linalg.norm(u) if np.linalg.norm(u) > 0 else np.array([0.0, 1.0, 0.0])
-        q = c[i] + u * r[i] * (1 + rng.choice([-1e-6, 0.0, 1e-7, 3e-7, 1e-6, 1e-5]))
+        a, sgn = rng.integers(0, 3), rng.choice([-1.0, 1.0])
+        i = np.argmax(sgn * c[:, a] + r)
+        e = np.zeros(3)
+        e[a] = sgn
+        q = c[i] + e * r[i] * (1 + rng.choice([-1e-6, 0.0, 1e-7, 3e-7, 1e-6, 1e-5]))
         p = rng.normal(size=3)
-        p -= (p @ u) * u
+        p -= (p @ e) * e
         p /= np.linalg.norm(p)
         os_.append(q - rng.uniform(0.5, 40.0) * p)
         ds_.append(p * rng.choice([0.01, 1.0, 100.0]))
@@ -149,13 +175,15 @@ def test_groups_partition_the_scene(name):
             if gi < nb:
                 continue
             h = gi - nb
-            # the bound covers the member: Rk >= R (float64 geometry), and so do the node's
-            # and the chunk's
+            # the group's box holds the member (float64 geometry), and so do the node's and
+            # the chunk's; their K covers its radius
+            c = sp["center"][j].astype(np.float64)
+            r = abs(float(sp["radius"][j]))
             for tab, i in (("bound", h), ("node", h // 8), ("top", h // 64)):
-                e, b = i % 2, t[tab][i // 2]
-                C = np.array([b[0 + e], b[2 + e], b[4 + e]], np.float64)
-                dist = np.linalg.norm(sp["center"][j].astype(np.float64) - C)
-                assert dist + abs(float(sp["radius"][j])) <= float(b[8 + e]), (tab, i)
+                e, b = i % 2, t[tab][i // 2].astype(np.float64)
+                lo, hi = b[[0 + e, 2 + e, 4 + e]], b[[6 + e, 8 + e, 10 + e]]
+                assert (lo <= c - r).all() and (hi >= c + r).all(), (tab, i)
+                assert b[12 + e] >= 8.1 * 2.0 ** -24 / r, (tab, i)
 
 
 def test_small_or_unbounded_scenes_do_not_cull():
@@ -176,6 +204,7 @@ def test_bound_test_is_conservative(name):
     chunks = [grazing_rays(sp, 1500, rng) for _ in range(3)]
     chunks += [tangent_rays(sp, t, 1500, rng) for _ in range(2)]
     chunks += [random_rays(1500, rng, -20.0, 20.0), random_rays(500, rng, -2.0, 2.0)]
+    chunks += [random_rays(500, rng, -3000.0, 3000.0)]  # far origins: large margins
     for o, d in chunks:
         culled = group_culled(t, o, d, rng=rng)
         disc = member_disc(t, o, d)
@@ -193,17 +222,24 @@ def test_bound_test_is_conservative(name):
         total_culled += int(culled.sum())
         total += culled.size
     # and the test does cull (most groups are far from most rays)
-    assert total_culled > 0.5 * total
+    assert total_culled > 0.7 * total
 
 
-def test_checker_detects_a_too_small_bound():
-    """The emulated check above has teeth: bounds shrunk by 1% are caught."""
+def test_checker_detects_a_too_small_box():
+    """The emulated check above has teeth: boxes shrunk by 1e-4 of their size with no margin
+    are caught by the grazing rays."""
     rng = np.random.default_rng(11)
     sp = S.builtin_scene("final")
     t = S.cull_tables(sp)
     bad_t = {k: (v.copy() if hasattr(v, "copy") else v) for k, v in t.items()}
-    bad_t["bound"][:, 6:8] = 0                   # no margin
-    bad_t["bound"][:, 8:10] *= f32(0.99)         # radius 1% short
+    b = bad_t["bound"]
+    for k in range(3):
+        lo, hi = b[:, 2 * k:2 * k + 2], b[:, 6 + 2 * k:8 + 2 * k]
+        shrink = (hi - lo) * f32(1e-4)
+        b[:, 2 * k:2 * k + 2], b[:, 6 + 2 * k:8 + 2 * k] = lo + shrink, hi - shrink
+    b[:, 12:14] = 0                          # no per-box margin
+    bad_t["margin"] = t["margin"].copy()
+    bad_t["margin"][2] = 0                   # no rounding slack
     o, d = tangent_rays(sp, t, 1500, rng)
     culled = group_culled(bad_t, o, d)
     hit = ~(member_disc(t, o, d) < 0) & (t["index"][t["nbig"]:] >= 0)[None]
@@ -211,32 +247,43 @@ def test_checker_detects_a_too_small_bound():
 
 
 def test_margin_constants():
-    """K and Rk as tracer.hip derives them: K >= 32.4u / r_min (1 + 1e-5) + 6e-6 / (2R) and
-    Rk >= (R + 1.5 Kc R^2)(1 + 1e-5) with R the covering radius."""
+    """The host constants of the box test (cluster.cpp, tracer.hip (3)): per box K >= 8.1u /
+    r_min (1 + 1e-5) of its members; margin = (>= max |centre|, >= r_max^2, >= max |box
+    coordinate|) over the hierarchy."""
     sp = S.builtin_scene("final")
     t = S.cull_tables(sp)
     u = 2.0 ** -24
     nb = t["nbig"]
-    for gi in range(t["geom"].shape[0] - nb):
-        m = t["index"][nb + gi][t["index"][nb + gi] >= 0]
+    hier = t["index"][nb:]
+    m_all = hier[hier >= 0]
+    c = sp["center"][m_all].astype(np.float64)
+    r = np.abs(sp["radius"][m_all].astype(np.float64))
+    cmax, rmax2, lam = (float(v) for v in t["margin"][:3])
+    assert cmax >= np.linalg.norm(c, axis=1).max()
+    assert rmax2 >= (r ** 2).max()
+    assert lam >= (np.abs(c) + r[:, None]).max()
+    for gi in range(hier.shape[0]):
+        m = hier[gi][hier[gi] >= 0]
         if len(m) == 0:
             continue
         e, bb = gi % 2, t["bound"][gi // 2]
-        C = bound_of(t, gi)
-        r = np.abs(sp["radius"][m].astype(np.float64))
-        R = (np.linalg.norm(sp["center"][m].astype(np.float64) - C, axis=1) + r).max()
-        Kc = 32.4 * u / r.min()
-        assert float(bb[6 + e]) >= Kc * (1 + 1e-5) + 6e-6 / (2 * R * (1 + 1e-6))
-        assert float(bb[8 + e]) >= (R + 1.5 * Kc * R * R) * (1 + 1e-5)
+        rm = np.abs(sp["radius"][m].astype(np.float64)).min()
+        assert float(bb[12 + e]) >= 8.1 * u / rm * (1 + 1e-5)
 
 
 def test_hierarchy_is_aligned():
-    """Nodes (8 groups) and chunks (64 groups) are whole k-d subtrees: a node's bound is no
-    larger than the union of its groups' bounds needs (sanity: node radius <= 4x median group
-    radius on the grid scenes)."""
+    """Nodes (8 groups) and chunks (64 groups) are whole k-d subtrees: a node's box is not much
+    larger than its groups' (sanity: median node diagonal <= 4x the median group diagonal on
+    the grid scenes)."""
     for name in ("final", "stress4096"):
         t = S.cull_tables(S.builtin_scene(name))
-        gR = np.concatenate([t["bound"][:, 8], t["bound"][:, 9]])
-        nR = np.concatenate([t["node"][:, 8], t["node"][:, 9]])
-        real = nR > 0
-        assert np.median(nR[real]) <= 4 * np.median(gR[gR > 0])
+
+        def diag(tab):
+            b = tab.astype(np.float64)
+            out = []
+            for e in (0, 1):
+                lo, hi = b[:, [0 + e, 2 + e, 4 + e]], b[:, [6 + e, 8 + e, 10 + e]]
+                out.append(np.linalg.norm(hi - lo, axis=1))
+            dd = np.concatenate(out)
+            return dd[dd > 0]
+        assert np.median(diag(t["node"])) <= 4 * np.median(diag(t["bound"]))

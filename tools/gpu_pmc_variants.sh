@@ -7,7 +7,7 @@ ROOT=$GRAFT_REPO_ROOT
 cd /tmp
 for v in ${VARIANTS_PMC:-2 3 4}; do
   timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $ROOT/gpurun_out/pmcv/v${v}_a -o run -- python3 $ROOT/tools/render_once.py --spp 64 --variant $v > $ROOT/gpurun_out/pmcv/v${v}_a.log 2>&1 || exit 1
-  timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS --output-format csv -d $ROOT/gpurun_out/pmcv/v${v}_b -o run -- python3 $ROOT/tools/render_once.py --spp 64 --variant $v > $ROOT/gpurun_out/pmcv/v${v}_b.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --output-format csv -d $ROOT/gpurun_out/pmcv/v${v}_b -o run -- python3 $ROOT/tools/render_once.py --spp 64 --variant $v > $ROOT/gpurun_out/pmcv/v${v}_b.log 2>&1 || exit 1
 done
 cd $ROOT
 VARIANTS_PMC="${VARIANTS_PMC:-2 3 4}" python3 - <<'PY'

@@ -65,6 +65,7 @@ struct RendererState {
     float* d_material = nullptr;
     // culled-scan tables (cluster.hpp); ncgroups == 0 when culling does not apply
     int32_t ncgroups = 0, ncbig = 0;
+    float cmargin[4] = {0, 0, 0, 0};  // box margin constants (CullTables::margin)
     float4* d_cgroup = nullptr;
     float4* d_cbound = nullptr;
     float4* d_cnode = nullptr;
@@ -453,6 +454,7 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
                            hipMemcpyHostToDevice));
         g.ncgroups = ct.ngroups;
         g.ncbig = ct.nbig;
+        std::memcpy(g.cmargin, ct.margin, sizeof(ct.margin));
     }
     VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float) * table.size()));
     VCRT_TRY(hipMemcpy(g.d_geom, table.data(), sizeof(float) * table.size(),
@@ -523,6 +525,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.ctop = g.d_ctop;
         p.ncgroups = g.ncgroups;
         p.nbig = g.ncbig;
+        for (int k = 0; k < 4; k++) p.box_margin[k] = g.cmargin[k];
         p.nspheres = g.nspheres;
         p.width = g.desc.width;
         p.height = g.desc.height;
@@ -548,18 +551,19 @@ vcrt_result vcrt_draw_next_frame(void) {
         // per-lane culled scan: tables in LDS. Up to 32 KB with 256-thread workgroups (5 per
         // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
         // copy for 16 waves); beyond that from global memory.
-        const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 3 + g.ncgroups * 5));
+        const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
         const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
         const bool lane_wide = lane_lds && tab_lds > 32768u;
         int variant = g.desc.kernel_variant;
-        // Measured on MI355X: of the linear scans the scalar-cache variant (sphere data in
-        // SGPRs, no LDS traffic) beats LDS staging by 15% (485 spheres) and 18% (4100); the
-        // culled scans beat both (same bits). AUTO: the per-lane culled scan (485 spheres,
-        // tables in LDS: 2.5x SMEM, +27% over CULL; 4100 spheres, tables in global memory:
-        // 1.9x SMEM, +4% over CULL), and SMEM when the scene has no tables (< 16 spheres or
-        // unbounded).
+        // Measured on MI355X (1080p, box hierarchy): of the linear scans the scalar-cache
+        // variant (sphere data in SGPRs, no LDS traffic) beats LDS staging by 15% (485
+        // spheres) and 18% (4100); the culled scans beat both (same bits). AUTO: the flattened
+        // scan when its tables fit in LDS beside its stacks (485 spheres: 3.3x SMEM, +14%
+        // over CULL_LANE, +28% over CULL), else the per-lane scan (4100 spheres, 1024-thread
+        // blocks: 6.2x SMEM, level with CULL), and SMEM when the scene has no tables (< 16
+        // spheres or unbounded).
         if (variant == VCRT_KERNEL_AUTO)
-            variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_LANE;
+            variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_FLAT;
         if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
         if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE ||
              variant == VCRT_KERNEL_CULL_FLAT) &&
@@ -567,7 +571,9 @@ vcrt_result vcrt_draw_next_frame(void) {
             variant = VCRT_KERNEL_SMEM;
         // the flattened exact phase needs its tables in LDS beside 3.5 KB of scratch per wave
         constexpr uint32_t kFlatScratch = 4 * vcrt::kWaveScratchBytes;  // 4 waves per block
-        if (variant == VCRT_KERNEL_CULL_FLAT && (!lane_lds || lane_wide)) variant = VCRT_KERNEL_CULL_LANE;
+        if (variant == VCRT_KERNEL_CULL_FLAT &&
+            (!lane_lds || lane_wide || g.ncgroups > vcrt::kFlatMaxGroups))
+            variant = VCRT_KERNEL_CULL_LANE;
         hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
         uint32_t lds = 0;
         if (variant == VCRT_KERNEL_LDS) {
@@ -802,11 +808,12 @@ size_t vcrt_scene_generator_text(char* buf, size_t cap) {
 
 int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom, float* bound,
                          float* node, float* top, int32_t* index, int32_t* big_groups,
-                         int32_t cap_groups) {
+                         float* margin4, int32_t cap_groups) {
     if (count < 0 || (count > 0 && !spheres)) return 0;
     vcrt::CullTables ct;
     if (!vcrt::build_cull_tables(spheres, count, ct)) return 0;
     if (big_groups) *big_groups = ct.nbig;
+    if (margin4) std::memcpy(margin4, ct.margin, sizeof(ct.margin));
     if (ct.nbig + ct.ngroups <= cap_groups) {
         if (geom) std::memcpy(geom, ct.geom.data(), sizeof(float) * ct.geom.size());
         if (bound) std::memcpy(bound, ct.bound.data(), sizeof(float) * ct.bound.size());

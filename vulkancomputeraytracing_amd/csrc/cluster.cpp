@@ -1,4 +1,4 @@
-// cluster.cpp -- k-d grouping of spheres into fours + conservative group bounds (cluster.hpp).
+// cluster.cpp -- k-d grouping of spheres into fours + conservative group boxes (cluster.hpp).
 #include "cluster.hpp"
 
 #include <algorithm>
@@ -57,70 +57,55 @@ void split(std::vector<int32_t>& idx, size_t lo, size_t hi, const vcrt_sphere* s
     split(idx, mid, hi, s, groups);
 }
 
-constexpr double kU = 0x1p-24;           // fp32 unit roundoff
-constexpr double kKcNum = 32.4 * kU;       // Kc = kKcNum / r_min (tracer.hip, (2))
-constexpr double kRel = 1e-5;              // relative slack of the bound test
-constexpr double kAbs = 6e-6;              // evaluation slack * |oC|^2 (> 35u)
+constexpr double kU = 0x1p-24;  // fp32 unit roundoff
 
-struct Bound {
-    float C[3] = {3.0e8f, 3.0e8f, 3.0e8f};  // padding: far away, zero size (K = Rk = 0)
-    float K = 0.f, Rk = 0.f;                // the lane test: RM = K |oC|^2 + Rk
+// Smallest float <= x (x finite, double).
+float round_down(double x) {
+    float f = static_cast<float>(x);
+    if (static_cast<double>(f) > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+
+struct Box {
+    float lo[3] = {1e20f, 1e20f, 1e20f};  // padding: a point far away (its groups are empty)
+    float hi[3] = {1e20f, 1e20f, 1e20f};
+    float K = 0.0f;                       // margin factor 8.1u / r_min of the members
 };
 
-// Bound of `members`: centre of their box (rounded to fp32 first), radius R covering every
-// member from that fp32 centre (+1e-6 relative), margin Kc = 32.4u / r_min, and the kernel's
-// constants K = Kc (1 + 1e-5) + 6e-6 / (2R), Rk = (R + 1.5 Kc R^2)(1 + 1e-5), rounded up
-// (tracer.hip). r_min < 1e-3: K = inf, never culled. No members (padding): a zero-size bound
-// far away, culled by every ray not aimed straight at it (harmless: its groups are empty).
-Bound bound_of(const vcrt_sphere* s, const std::vector<int32_t>& members) {
-    Bound b;
+// Axis-aligned box of `members` (centre -+ |radius|, rounded outwards to fp32) and its margin
+// factor K = 8.1u / r_min (1 + 1e-5), rounded up (inf for a zero radius: never ruled out).
+Box box_of(const vcrt_sphere* s, const std::vector<int32_t>& members) {
+    Box b;
     if (members.empty()) return b;
-    double lo[3], hi[3];
-    for (int a = 0; a < 3; a++) {
-        lo[a] = std::numeric_limits<double>::infinity();
-        hi[a] = -lo[a];
-    }
     double rmin = std::numeric_limits<double>::infinity();
-    for (int32_t j : members) {
-        const double r = std::fabs(static_cast<double>(s[j].radius));
-        rmin = std::min(rmin, r);
-        for (int a = 0; a < 3; a++) {
-            lo[a] = std::min(lo[a], s[j].center[a] - r);
-            hi[a] = std::max(hi[a], s[j].center[a] + r);
+    for (int32_t j : members) rmin = std::min(rmin, std::fabs(static_cast<double>(s[j].radius)));
+    b.K = rmin > 0.0 ? round_up(std::min(8.1 * kU / rmin * (1.0 + 1e-5), 1e38))
+                     : std::numeric_limits<float>::infinity();
+    for (int a = 0; a < 3; a++) {
+        double lo = std::numeric_limits<double>::infinity(), hi = -lo;
+        for (int32_t j : members) {
+            const double r = std::fabs(static_cast<double>(s[j].radius));
+            lo = std::min(lo, s[j].center[a] - r);
+            hi = std::max(hi, s[j].center[a] + r);
         }
+        b.lo[a] = round_down(lo);
+        b.hi[a] = round_up(hi);
     }
-    for (int a = 0; a < 3; a++) b.C[a] = static_cast<float>(0.5 * (lo[a] + hi[a]));
-    double rad = 0.0;
-    for (int32_t j : members) {
-        double d2 = 0.0;
-        for (int a = 0; a < 3; a++) {
-            const double d = static_cast<double>(s[j].center[a]) - b.C[a];
-            d2 += d * d;
-        }
-        rad = std::max(rad, std::sqrt(d2) + std::fabs(static_cast<double>(s[j].radius)));
-    }
-    const double R = std::max(rad * (1.0 + 1e-6), 1e-30);
-    if (rmin < 1e-3) {
-        b.K = std::numeric_limits<float>::infinity();
-        b.Rk = round_up(R);
-        return b;
-    }
-    const double Kc = kKcNum / rmin;
-    b.K = round_up(Kc * (1.0 + kRel) + kAbs / (2.0 * R));
-    b.Rk = round_up((R + 1.5 * Kc * R * R) * (1.0 + kRel));
     return b;
 }
 
-// Element i of a pair-SoA bound table (TraceParams.cbound):
-//   (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1) (Rk0,Rk1,0,0)
-void put_bound(std::vector<float>& table, size_t i, const Bound& b) {
-    float* t = &table[(i / 2) * 12];
+// Element i of a pair-SoA box table (TraceParams.cbound / cnode / ctop):
+//   (lox0,lox1,loy0,loy1) (loz0,loz1,hix0,hix1) (hiy0,hiy1,hiz0,hiz1) (K0,K1,0,0)
+void put_box(std::vector<float>& table, size_t i, const Box& b) {
+    float* t = &table[(i / 2) * 16];
     const int e = i % 2;
-    t[0 + e] = b.C[0];
-    t[2 + e] = b.C[1];
-    t[4 + e] = b.C[2];
-    t[6 + e] = b.K;
-    t[8 + e] = b.Rk;
+    t[0 + e] = b.lo[0];
+    t[2 + e] = b.lo[1];
+    t[4 + e] = b.lo[2];
+    t[6 + e] = b.hi[0];
+    t[8 + e] = b.hi[1];
+    t[10 + e] = b.hi[2];
+    t[12 + e] = b.K;
 }
 
 }  // namespace
@@ -175,8 +160,8 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
     out.ngroups = static_cast<int32_t>(ng);
     out.geom.assign(nall * 16, 0.0f);
     out.index.assign(nall * 4, -1);
-    out.bound.assign(ng / 2 * 12, 0.0f);
-    out.node.assign(ng / kNodeGroups / 2 * 12, 0.0f);
+    out.bound.assign(ng / 2 * 16, 0.0f);
+    out.node.assign(ng / kNodeGroups / 2 * 16, 0.0f);
     for (size_t gi = 0; gi < nall; gi++) {
         const Group& g = gi < nbig ? bigg[gi] : groups[gi - nbig];
         // members: pair-SoA exactly as the linear table (r^2 = radius * radius in fp32)
@@ -205,13 +190,30 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
                 if (groups[gi][k] >= 0) m.push_back(groups[gi][k]);
         return m;
     };
-    for (size_t gi = 0; gi < ng; gi++) put_bound(out.bound, gi, bound_of(s, members_of(gi, gi + 1)));
+    for (size_t gi = 0; gi < ng; gi++) put_box(out.bound, gi, box_of(s, members_of(gi, gi + 1)));
     for (size_t ni = 0; ni < ng / kNodeGroups; ni++)
-        put_bound(out.node, ni, bound_of(s, members_of(ni * kNodeGroups, (ni + 1) * kNodeGroups)));
-    // top level: one bound per chunk of 64 groups (the kernels' unit of work per pass)
+        put_box(out.node, ni, box_of(s, members_of(ni * kNodeGroups, (ni + 1) * kNodeGroups)));
+    // top level: one box per chunk of 64 groups (the kernels' unit of work per pass)
     const size_t nt = (ng + 63) / 64, nt2 = nt + (nt & 1);
-    out.top.assign(nt2 / 2 * 12, 0.0f);
-    for (size_t ti = 0; ti < nt2; ti++) put_bound(out.top, ti, bound_of(s, members_of(ti * 64, ti * 64 + 64)));
+    out.top.assign(nt2 / 2 * 16, 0.0f);
+    for (size_t ti = 0; ti < nt2; ti++) put_box(out.top, ti, box_of(s, members_of(ti * 64, ti * 64 + 64)));
+    // the per-ray margin constants (tracer.hip, box_ray) over the hierarchy's spheres
+    double rmax = 0.0, cmax = 0.0, lam = 0.0;
+    for (int32_t j : normal) {
+        const double r = std::fabs(static_cast<double>(s[j].radius));
+        rmax = std::max(rmax, r);
+        double c2 = 0.0;
+        for (int a = 0; a < 3; a++) {
+            const double c = s[j].center[a];
+            c2 += c * c;
+            lam = std::max(lam, std::fabs(c) + r);
+        }
+        cmax = std::max(cmax, std::sqrt(c2));
+    }
+    out.margin[0] = round_up(cmax * (1.0 + 1e-6));
+    out.margin[1] = round_up(rmax * rmax * (1.0 + 1e-6));
+    out.margin[2] = round_up(lam * (1.0 + 1e-6));
+    out.margin[3] = 0.0f;
     return true;
 }
 

@@ -3,7 +3,8 @@
 // The reference scans world[] linearly for every ray (functions.glsl:77-81). Because that scan
 // picks the smallest accepted t with ties to the earliest index (tracer.hip, scan_culled), the
 // spheres can be visited in any order; this module reorders them into spatially compact groups
-// of four with conservative bounding spheres so a wave can skip groups no lane's ray comes near.
+// of four with conservative axis-aligned boxes so a wave can skip groups no lane's ray comes
+// near.
 #pragma once
 
 #include <cstdint>
@@ -13,17 +14,19 @@
 
 namespace vcrt {
 
-constexpr int kNodeGroups = 8;  // groups per node of the bound hierarchy
+constexpr int kNodeGroups = 8;  // groups per node of the box hierarchy
 
 struct CullTables {
     int32_t nbig = 0;             // big-sphere groups, first in geom/index, tested for every ray
     int32_t ngroups = 0;          // hierarchy groups after them, a multiple of 2 * kNodeGroups
     std::vector<float> geom;      // [nbig + ngroups][16] pair-SoA, same values as the linear table
     std::vector<int32_t> index;   // [nbig + ngroups][4] world[] index of each member, -1 = padding
-    std::vector<float> bound;     // [ngroups / 2][12] hierarchy group-pair bounds (TraceParams)
-    std::vector<float> node;      // [ngroups / kNodeGroups / 2][12] node-pair bounds, same form
-    std::vector<float> top;       // [ceil(ngroups / 64) rounded up to even / 2][12] bounds of
+    std::vector<float> bound;     // [ngroups / 2][16] hierarchy group-pair boxes (TraceParams)
+    std::vector<float> node;      // [ngroups / kNodeGroups / 2][16] node-pair boxes, same form
+    std::vector<float> top;       // [ceil(ngroups / 64) rounded up to even / 2][16] boxes of
                                   // each 64-group chunk (8 nodes), same form
+    float margin[4] = {0, 0, 0, 0};  // box-test constants over the hierarchy: max |centre|,
+                                     // r_max^2, max |coordinate| of a box (rounded up), 0
 };
 
 // Builds the grouped tables. Returns false (tables empty) when culling does not apply: fewer

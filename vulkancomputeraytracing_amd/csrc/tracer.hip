@@ -180,14 +180,24 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
 //      difference) implies that the ray line passes within r + M_s of the centre,
 //      M_s = 8.1u (|oc|^2 + r^2) / r: the roundings move hb^2 - a*cc by at most ~15u a |oc|^2
 //      and the rounded oc moves the centre by u |oc|. For a bound (C, R) of members with
-//      radius >= r_min, |oc|^2 + r^2 <= 2 |oC|^2 + 3 R^2, so M = Kc (|oC|^2 + 1.5 R^2) with
-//      Kc = 32.4u / r_min covers every member twice over.
-// Bound test, per lane: with the approximate unit direction w = d * rsq(a) (|w| = 1 + O(10u))
-// and h = (o - C).w, X = |oC|^2 - h^2 approximates the squared line distance within 35u |oC|^2
-// (rounded oc, w, h, |oC|^2, X). The lane rules the bound out when X > RM^2 with
-//   RM = K |oC|^2 + Rk,  K = Kc (1 + 1e-5) + 6e-6 / (2R),  Rk = (R + 1.5 Kc R^2)(1 + 1e-5)
-// (host constants, rounded up), since RM^2 >= (R + M)^2 (1 + 2e-5) + 6e-6 |oC|^2 and 6e-6 > 35u:
-// the line then misses every member by more than its margin, so no member has disc_f >= 0.
+//      box's members (radius >= r_b, all |c| <= c_max, r <= r_max) M_s <= M_b = K_b Q with
+//      K_b = 8.1u / r_b and Q = (|o| + c_max)^2 + r_max^2.
+//  (3) the box test. Group, node and chunk bounds are axis-aligned boxes B = [lo, hi] of their
+//      members (rounded outwards) with their K_b. Per axis the lane computes the plane
+//      parameters fma(lo, inv, c), fma(hi, inv, c) with inv = v_rcp(d') (1 ulp), c = -o inv,
+//      d' = d with components below 2^-40 raised to 2^-40; tnear = max of the per-axis minima,
+//      tfar = min of the maxima, and rules B out when
+//        gap = fma(K_b, c2, (tfar - tnear) + c1) < 0,
+//        c1 = 1.001 J 5.1u (L + |o|_inf),  c2 = 1.001 J Q,  J = 2 max_i |inv_i|,
+//      L = max |box coordinate|. Why: if the real line met B grown by M_b at t*, every exact
+//      per-axis interval of B would reach within (M_b + dc) / |d'_i| of t*, where dc <=
+//      sqrt(3) 2^-30 (L + M_b + |o|_inf) bounds the shift from d to d' (a >= 2^-20); each
+//      computed end lies within 4.02u (L + |o_i|) / |d'_i| of its exact value (rcp 2u, two
+//      roundings); and 1 / |d'_i| <= (1 + 2.01u) J / 2. So tfar - tnear >= -(M_b + dc + 4.02u
+//      (L + |o|_inf)) (1 + 2.01u) J, which c1 + K_b c2 exceeds by more than the last three
+//      roundings: gap >= 0, the box is kept. Hence a ruled-out box holds no member with
+//      disc_f >= 0. (Q and the 1.001 factors absorb the per-ray roundings; K_b = inf, a zero
+//      radius, keeps its box.) The host passes K_b, c_max, r_max^2 and L rounded up.
 // Waves holding a ray outside the guarded range scan the original table in reference order.
 
 // t of one candidate as hit_sphere would accept it (finite case, fact (1)).
@@ -240,40 +250,78 @@ __device__ __forceinline__ uint32_t nonzero(uint64_t x) {
     return r;
 }
 
-struct CullRay {  // one ray, splatted for packed tests
-    v2f ox, oy, oz;  // origin
-    v2f wx, wy, wz;  // approximate unit direction
+struct CullRay {  // one ray's origin, splatted for packed tests
+    v2f ox, oy, oz;
 };
 
-// Bound test of one pair (TraceParams.cbound: (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1)
-// (Rk0,Rk1,-,-)): bit 0/1 set when some lane may accept a member of bound 0/1 (NaN compares as
-// "may").
+// One ray prepared for the box test (3), splatted for packed tests.
+struct BoxRay {
+    v2f ix, iy, iz;  // 1 / d'
+    v2f cx, cy, cz;  // -o / d'
+    v2f c1, c2;      // gap slack: c1 + K_b c2
+};
+
+__device__ __forceinline__ float box_axis(float o, float d, v2f& i, v2f& c) {
+    const float dd = copysignf(fmaxf(fabsf(d), 0x1p-40f), d);
+    const float iv = __builtin_amdgcn_rcpf(dd);
+    const float co = -o * iv;
+    i = (v2f){iv, iv};
+    c = (v2f){co, co};
+    return fabsf(iv);
+}
+
+__device__ __forceinline__ BoxRay box_ray(const TraceParams& p, const f3 o, const f3 d) {
+    BoxRay r;
+    const float ax = box_axis(o.x, d.x, r.ix, r.cx), ay = box_axis(o.y, d.y, r.iy, r.cy),
+                az = box_axis(o.z, d.z, r.iz, r.cz);
+    const float J = 2.002f * fmaxf(fmaxf(ax, ay), az);  // 1.001 J
+    const float on = __builtin_amdgcn_sqrtf(dot(o, o)) + p.box_margin[0];
+    const float Q = on * on + p.box_margin[1];
+    const float oinf = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float c1 = J * (3.04e-7f * (p.box_margin[2] + oinf));  // 5.1u
+    const float c2 = J * Q;
+    r.c1 = (v2f){c1, c1};
+    r.c2 = (v2f){c2, c2};
+    return r;
+}
+
+// The box test's gap for a pair of boxes (TraceParams.cbound: (lox0,lox1,loy0,loy1)
+// (loz0,loz1,hix0,hix1) (hiy0,hiy1,hiz0,hiz1) (K0,K1,-,-)): negative when the ray rules the box
+// out. (All values finite or +inf, so the gap is never -0 or NaN.)
+__device__ __forceinline__ v2f box_gap(const BoxRay& r, float4 b0, float4 b1, float4 b2,
+                                       float4 b3) {
+    const v2f lox = {b0.x, b0.y}, loy = {b0.z, b0.w}, loz = {b1.x, b1.y};
+    const v2f hix = {b1.z, b1.w}, hiy = {b2.x, b2.y}, hiz = {b2.z, b2.w}, K = {b3.x, b3.y};
+    const v2f tlx = vfma(lox, r.ix, r.cx), thx = vfma(hix, r.ix, r.cx);
+    const v2f tly = vfma(loy, r.iy, r.cy), thy = vfma(hiy, r.iy, r.cy);
+    const v2f tlz = vfma(loz, r.iz, r.cz), thz = vfma(hiz, r.iz, r.cz);
+    v2f tn, tf;
+    tn.x = fmaxf(fmaxf(fminf(tlx.x, thx.x), fminf(tly.x, thy.x)), fminf(tlz.x, thz.x));
+    tn.y = fmaxf(fmaxf(fminf(tlx.y, thx.y), fminf(tly.y, thy.y)), fminf(tlz.y, thz.y));
+    tf.x = fminf(fminf(fmaxf(tlx.x, thx.x), fmaxf(tly.x, thy.x)), fmaxf(tlz.x, thz.x));
+    tf.y = fminf(fminf(fmaxf(tlx.y, thx.y), fmaxf(tly.y, thy.y)), fmaxf(tlz.y, thz.y));
+    return vfma(K, r.c2, (tf - tn) + r.c1);
+}
+
+// Box test of one pair, wave-uniform: bit 0/1 set when some lane may accept a member of box
+// 0/1.
 struct BoundPair {
-    float4 b0, b1;
-    float2 b2;
+    float4 b0, b1, b2, b3;
 };
 
 __device__ __forceinline__ BoundPair load_bound_pair(cfloat4* b) {
-    return BoundPair{b[0], b[1], *(__attribute__((address_space(4))) const float2*)(b + 2)};
+    return BoundPair{b[0], b[1], b[2], b[3]};
 }
 
 template <bool kStats>
-__device__ __forceinline__ uint32_t bound_pair_need(const CullRay& r, const BoundPair& bp,
+__device__ __forceinline__ uint32_t bound_pair_need(const BoxRay& r, const BoundPair& bp,
                                                     uint32_t& lane_needs, uint32_t& lane_cnt) {
-    const float4 b0 = bp.b0, b1 = bp.b1;
-    const float2 b2 = bp.b2;
-    const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y};
-    const v2f K = {b1.z, b1.w}, Rk = {b2.x, b2.y};
-    const v2f ocx = r.ox - Cx, ocy = r.oy - Cy, ocz = r.oz - Cz;
-    const v2f oc2 = vfma(ocz, ocz, vfma(ocy, ocy, ocx * ocx));
-    const v2f h = vfma(ocz, r.wz, vfma(ocy, r.wy, ocx * r.wx));
-    const v2f X = vfma(-h, h, oc2);   // ~ squared line distance
-    const v2f RM = vfma(K, oc2, Rk);  // >= R + M, with the slack folded in
-    const v2f T = RM * RM;
-    const uint64_t n0 = __ballot(!(X.x > T.x)), n1 = __ballot(!(X.y > T.y));
+    const v2f g = box_gap(r, bp.b0, bp.b1, bp.b2, bp.b3);
+    const bool m0 = !(g.x < 0.0f), m1 = !(g.y < 0.0f);
+    const uint64_t n0 = __ballot(m0), n1 = __ballot(m1);
     if constexpr (kStats) {
         lane_needs += __popcll(n0) + __popcll(n1);
-        lane_cnt += (uint32_t)!(X.x > T.x) + (uint32_t)!(X.y > T.y);
+        lane_cnt += (uint32_t)m0 + (uint32_t)m1;
     }
     return nonzero(n0) | (nonzero(n1) << 1);
 }
@@ -310,14 +358,11 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
                                             uint32_t& lane_cnt) {
     uint32_t node_lanes = 0, node_cnt = 0;
     const float a = dot(d, d);
-    const float inv = __builtin_amdgcn_rsqf(a);
     CullRay r;
     r.ox = (v2f){o.x, o.x};
     r.oy = (v2f){o.y, o.y};
     r.oz = (v2f){o.z, o.z};
-    r.wx = (v2f){d.x * inv, d.x * inv};
-    r.wy = (v2f){d.y * inv, d.y * inv};
-    r.wz = (v2f){d.z * inv, d.z * inv};
+    const BoxRay br = box_ray(p, o, d);
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     cfloat4* bound = (cfloat4*)p.cbound;
     cfloat4* node = (cfloat4*)p.cnode;
@@ -332,7 +377,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     for (int base = 0; base < ncg; base += 64) {
         // level 0: the chunk's own bound (tested for two chunks at a time)
         if ((base & 127) == 0) {
-            tops = bound_pair_need<false>(r, load_bound_pair(top + 3 * (base >> 7)), node_lanes,
+            tops = bound_pair_need<false>(br, load_bound_pair(top + 4 * (base >> 7)), node_lanes,
                                           node_cnt);
             bounds_tested += 2;
         }
@@ -340,27 +385,27 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
         // level 1: which of the next (up to) 8 nodes of 8 groups may any lane hit? (the
         // scalar loads run one pair ahead of the tests)
         const int nn = min(8, (ncg - base) >> 3);
-        cfloat4* nb = node + 3 * (base >> 4);
+        cfloat4* nb = node + 4 * (base >> 4);
         uint32_t nodes = 0;
         BoundPair cur = load_bound_pair(nb);
         for (int j = 0; j < nn; j += 2) {
-            const BoundPair nxt = load_bound_pair(nb + 3 * ((j + 2 < nn ? j + 2 : j) >> 1));
-            nodes |= bound_pair_need<false>(r, cur, node_lanes, node_cnt) << j;
+            const BoundPair nxt = load_bound_pair(nb + 4 * ((j + 2 < nn ? j + 2 : j) >> 1));
+            nodes |= bound_pair_need<false>(br, cur, node_lanes, node_cnt) << j;
             cur = nxt;
         }
         bounds_tested += (uint64_t)(nn + 8 * __popc(nodes));
         // level 2: which groups of those nodes?
         uint64_t need = 0;
-        if (nodes) cur = load_bound_pair(bound + 3 * ((base + 8 * __builtin_ctz(nodes)) >> 1));
+        if (nodes) cur = load_bound_pair(bound + 4 * ((base + 8 * __builtin_ctz(nodes)) >> 1));
         while (nodes) {
             const int j = __builtin_ctz(nodes);
             nodes &= nodes - 1;
-            cfloat4* gb = bound + 3 * ((base + 8 * j) >> 1);
-            cfloat4* gnext = bound + 3 * ((base + 8 * (nodes ? __builtin_ctz(nodes) : j)) >> 1);
+            cfloat4* gb = bound + 4 * ((base + 8 * j) >> 1);
+            cfloat4* gnext = bound + 4 * ((base + 8 * (nodes ? __builtin_ctz(nodes) : j)) >> 1);
 #pragma unroll
             for (int k = 0; k < 8; k += 2) {
-                const BoundPair nxt = load_bound_pair(k + 2 < 8 ? gb + 3 * ((k + 2) >> 1) : gnext);
-                need |= (uint64_t)bound_pair_need<kStats>(r, cur, hit_groups, lane_cnt)
+                const BoundPair nxt = load_bound_pair(k + 2 < 8 ? gb + 4 * ((k + 2) >> 1) : gnext);
+                need |= (uint64_t)bound_pair_need<kStats>(br, cur, hit_groups, lane_cnt)
                         << (8 * j + k);
                 cur = nxt;
             }
@@ -415,19 +460,11 @@ __device__ __forceinline__ uint32_t push_sign(uint32_t acc, float v) {
     return __builtin_amdgcn_alignbit(acc, __float_as_uint(v), 31);
 }
 
-// Sign of fma(RM, RM, -X) for both bounds of a pair: set (negative) when this lane rules the
-// bound out (X > RM^2 exactly; NaN -- an infinite K at |oC| = 0 -- keeps the default NaN's
-// clear sign bit, i.e. "may need"). Pushed high element first.
-__device__ __forceinline__ uint32_t push_bound_pair(uint32_t acc, const CullRay& r, float4 b0,
-                                                    float4 b1, float2 b2) {
-    const v2f Cx = {b0.x, b0.y}, Cy = {b0.z, b0.w}, Cz = {b1.x, b1.y};
-    const v2f K = {b1.z, b1.w}, Rk = {b2.x, b2.y};
-    const v2f ocx = r.ox - Cx, ocy = r.oy - Cy, ocz = r.oz - Cz;
-    const v2f oc2 = vfma(ocz, ocz, vfma(ocy, ocy, ocx * ocx));
-    const v2f h = vfma(ocz, r.wz, vfma(ocy, r.wy, ocx * r.wx));
-    const v2f X = vfma(-h, h, oc2);
-    const v2f RM = vfma(K, oc2, Rk);
-    const v2f D = vfma(RM, RM, -X);
+// Sign of the box gap for both boxes of a pair: set (negative) when this lane rules the box
+// out. Pushed high element first.
+__device__ __forceinline__ uint32_t push_bound_pair(uint32_t acc, const BoxRay& r, float4 b0,
+                                                    float4 b1, float4 b2, float4 b3) {
+    const v2f D = box_gap(r, b0, b1, b2, b3);
     return push_sign(push_sign(acc, D.y), D.x);
 }
 
@@ -437,20 +474,31 @@ __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
     return __uint_as_float((__float_as_uint(hb) | __float_as_uint(cc)) & ~__float_as_uint(disc));
 }
 
-// ---- flattened exact phase (variant CULL_FLAT) ----------------------------------------------
-// The per-lane exact loop runs as many passes as the wave's busiest lane needs groups (10 when
-// the mean lane needs 5). Here the wave's (lane, group) pairs are listed in LDS and dealt out
-// 64 per pass, each lane testing another lane's ray (fetched with ds_bpermute); candidate roots
-// are listed as well and resolved 64 at a time; every owner's (t, sphere index) minimum is kept
-// in an LDS 64-bit word updated with ds_min_u64 -- the lexicographic minimum of (t, index) is
-// exactly what `consider` computes, since t > 0 orders like its bit pattern.
-constexpr int kPairCap = 512;   // pairs per chunk and wave (more: per-lane loop instead)
-constexpr int kCandCap = 128;   // candidate roots listed before a resolve round
+// ---- flattened scan (variant CULL_FLAT) ------------------------------------------------------
+// The per-lane scan runs each level as many wave passes as its busiest lane needs (twice the
+// mean). Here the work items of the two per-lane levels and of the root evaluation are kept as
+// three per-wave stacks in LDS and dealt to the wave's live lanes a full wave at a time, each
+// lane working on another lane's ray (fetched with ds_bpermute):
+//   node  (owner, node)                -> tests the node's 8 group bounds -> group entries
+//   group (owner, group)               -> exact test of the 4 members     -> candidate entries
+//   cand  (owner, group, member)       -> the accepted root, into the owner's key
+// Entries are pushed at a wave prefix of the lanes' counts (their order never matters; stack
+// heights are wave-uniform, in SGPRs) and carried from chunk to chunk; only the segment's last
+// passes run partly empty. (A per-lane LDS atomic add on the height instead serialises on its
+// one address: 9x the LDS bank conflicts of the per-lane scan, 9% slower overall.) Every owner's
+// (t, sphere index) minimum is an LDS 64-bit word updated with ds_min_u64: the lexicographic
+// minimum of (t, index) is what `consider` computes, since t > 0 orders like its bit pattern.
+// Passes drain candidates first, then groups, then nodes, which bounds every stack:
+// < 64 left over + at most 8 x 64 (node, group) or 4 x 64 (cand) pushed by one pass.
+constexpr int kNodeCap = 576;
+constexpr int kGroupCap = 576;
+constexpr int kCandCap = 320;
 
 struct WaveScratch {
     unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
-    float4 cand[kCandCap];       // hb, disc, a, index | owner << 24
-    uint16_t pair[kPairCap];     // owner << 6 | group within the chunk
+    uint32_t cand[kCandCap];     // owner << 12 | group << 2 | member
+    uint16_t group[kGroupCap];   // owner << 10 | group
+    uint16_t node[kNodeCap];     // owner << 10 | node
 };
 static_assert(sizeof(WaveScratch) == kWaveScratchBytes, "host LDS size");
 
@@ -458,12 +506,13 @@ __device__ __forceinline__ unsigned long long pack_hit(float t, int idx) {
     return ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)idx;
 }
 
-// Exclusive prefix of a per-lane count c < 128 over the active lanes, and the wave total,
-// from bit-sliced ballots (inactive lanes count as 0).
+// Exclusive prefix over the active lanes of a per-lane count c < 2^kBits, and the wave total
+// (bit-sliced ballots: 4 VALU per bit).
+template <int kBits>
 __device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int b = 0; b < 7; ++b) {
+    for (int b = 0; b < kBits; ++b) {
         const uint64_t m = __ballot((c >> b) & 1u);
         pre += lanes_below(m) << b;
         tot += (uint32_t)__popcll(m) << b;
@@ -472,122 +521,239 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
     return pre;
 }
 
-// Resolve the listed candidate roots, 64 per pass, into the owners' keys.
-__device__ __forceinline__ void resolve_cands(WaveScratch* ws, uint32_t ncand, uint32_t rank,
-                                              uint32_t nact) {
-    for (uint32_t c0 = 0; c0 < ncand; c0 += nact) {
-        const uint32_t j = c0 + rank;
-        if (j < ncand) {
-            const float4 cd = ws->cand[j];
-            const float t = candidate_t(cd.x, cd.y, cd.z);
-            const uint32_t w = __float_as_uint(cd.w);
-            if (t > 0.001f && t < 1e5f)
-                atomicMin(&ws->key[w >> 24], pack_hit(t, (int)(w & 0xFFFFFFu)));
+// v of lane src_x4 / 4 (ds_bpermute; the source lane is live)
+__device__ __forceinline__ float from_lane(int src_x4, float v) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src_x4, __float_as_int(v)));
+}
+
+struct FlatRay {  // this lane's ray, as the passes fetch it
+    float ox, oy, oz, dx, dy, dz, a;
+    BoxRay br;
+};
+
+// One pass over the top min(n, nact) entries of a stack (n wave-uniform). kind 0: cand,
+// 1: group, 2: node. Lanes ranked past the entries run on their own ray and push nothing.
+// kKind 0: cand, 1: group, 2: node. n: this stack's height; pushed: the height of the stack
+// this pass pushes onto (group for node passes, cand for group passes).
+template <int kKind>
+__device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
+                                          uint32_t rank, uint32_t lane, WaveScratch* ws,
+                                          const float4* tbound, const float4* tgroup,
+                                          const FlatRay& my) {
+    const uint32_t m = min(n, nact), top = n - m;
+    n = top;
+    const bool act = rank < m;
+    if constexpr (kKind == 2) {  // node: the 8 group bounds of (owner, node)
+        const uint32_t e = act ? (uint32_t)ws->node[top + rank] : (lane << 10);
+        const int src = (int)(e >> 10) << 2;
+        BoxRay r;
+        const float ix = from_lane(src, my.br.ix.x), iy = from_lane(src, my.br.iy.x),
+                    iz = from_lane(src, my.br.iz.x);
+        const float cx = from_lane(src, my.br.cx.x), cy = from_lane(src, my.br.cy.x),
+                    cz = from_lane(src, my.br.cz.x);
+        const float c1 = from_lane(src, my.br.c1.x), c2 = from_lane(src, my.br.c2.x);
+        r.ix = (v2f){ix, ix};
+        r.iy = (v2f){iy, iy};
+        r.iz = (v2f){iz, iz};
+        r.cx = (v2f){cx, cx};
+        r.cy = (v2f){cy, cy};
+        r.cz = (v2f){cz, cz};
+        r.c1 = (v2f){c1, c1};
+        r.c2 = (v2f){c2, c2};
+        const float4* gb = tbound + __umul24(e & 1023u, 16u);
+        uint32_t gout = 0;
+#pragma unroll
+        for (int k = 3; k >= 0; k--)
+            gout = push_bound_pair(gout, r, gb[4 * k], gb[4 * k + 1], gb[4 * k + 2], gb[4 * k + 3]);
+        uint32_t need = act ? (~gout & 0xffu) : 0u;
+        uint32_t tot;
+        uint32_t pos = pushed + wave_prefix<4>((uint32_t)__popc(need), tot);
+        pushed += tot;
+        if (need) {
+            const uint32_t tag = (e & ~1023u) | ((e & 1023u) << 3);
+            do {
+                const uint32_t k = (uint32_t)__builtin_ctz(need);
+                need &= need - 1;
+                ws->group[pos++] = (uint16_t)(tag | k);
+            } while (need);
         }
+    } else if constexpr (kKind == 1) {  // group: exact test of the 4 members for the owner's ray
+        const uint32_t e = act ? (uint32_t)ws->group[top + rank] : (lane << 10);
+        const int src = (int)(e >> 10) << 2;
+        const float ox = from_lane(src, my.ox), oy = from_lane(src, my.oy), oz = from_lane(src, my.oz);
+        const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
+        const float a = from_lane(src, my.a);
+        const float4* g = tgroup + __umul24(e & 1023u, 5u);
+        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
+        const v2f vox = {ox, ox}, voy = {oy, oy}, voz = {oz, oz};
+        const v2f vdx = {dx, dx}, vdy = {dy, dy}, vdz = {dz, dz}, a2 = {a, a};
+        v2f hb01, cc01, d01, hb23, cc23, d23;
+        pair_disc_cc(vox, voy, voz, vdx, vdy, vdz, a2, q0, q1, hb01, cc01, d01);
+        pair_disc_cc(vox, voy, voz, vdx, vdy, vdz, a2, q2, q3, hb23, cc23, d23);
+        uint32_t hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
+        hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
+        hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
+        hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
+        hits = act ? hits : 0u;
+        uint32_t tot;
+        uint32_t pos = pushed + wave_prefix<3>((uint32_t)__popc(hits), tot);
+        pushed += tot;
+        if (hits) {
+            const uint32_t tag = e << 2;
+            do {
+                const uint32_t s = (uint32_t)__builtin_ctz(hits);
+                hits &= hits - 1;
+                ws->cand[pos++] = tag | s;
+            } while (hits);
+        }
+    } else {  // cand: the member's root (its hb, cc, disc recomputed as the packed test did)
+        const uint32_t e = act ? ws->cand[top + rank] : (lane << 12);
+        const int src = (int)(e >> 12) << 2;
+        const float ox = from_lane(src, my.ox), oy = from_lane(src, my.oy), oz = from_lane(src, my.oz);
+        const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
+        const float a = from_lane(src, my.a);
+        const uint32_t s = e & 3u;
+        const float4* g = tgroup + __umul24((e >> 2) & 1023u, 5u);
+        const float4 xy = g[(s >> 1) * 2], zr = g[(s >> 1) * 2 + 1], idf = g[4];
+        const bool hi = (s & 1u) != 0;
+        const float cx = hi ? xy.y : xy.x, cy = hi ? xy.w : xy.z;
+        const float cz = hi ? zr.y : zr.x, r2 = hi ? zr.w : zr.z;
+        const float ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+        const float hb = ocx * dx + ocy * dy + ocz * dz;
+        const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
+        const float disc = hb * hb - a * cc;
+        const float t = candidate_t(hb, disc, a);
+        const float ix = s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w;
+        if (act && t > 0.001f && t < 1e5f)
+            atomicMin(&ws->key[e >> 12], pack_hit(t, __float_as_int(ix)));
     }
 }
 
-// The exact test of this chunk's needed groups, flattened over the wave. Returns false (and
-// does nothing) when the wave needs more than kPairCap pairs in this chunk.
-__device__ __forceinline__ bool exact_flat(WaveScratch* ws, const float4* tg, uint64_t need,
-                                           const f3 o, const f3 d, float a, uint32_t lane,
-                                           uint32_t& n_passes) {
-    // only the wave's live lanes run this (finished lanes are masked off): pairs and
-    // candidates are dealt by rank among the live lanes, nact per pass
+// Runs passes while a stack holds at least `th` entries (th = nact: full passes only; 1: drain).
+struct FlatStacks {  // wave-uniform stack heights
+    uint32_t cand, group, node;
+};
+
+__device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
+                                           WaveScratch* ws, FlatStacks& h, const float4* tbound,
+                                           const float4* tgroup, const FlatRay& my,
+                                           uint32_t& n_groups, uint32_t& n_bounds) {
+    uint32_t nc = h.cand, ng = h.group, nn = h.node;
+    for (;;) {
+        __builtin_amdgcn_wave_barrier();  // the entries were written by other lanes
+        if (nc >= th) {
+            flat_pass<0>(nc, nc, nact, rank, lane, ws, tbound, tgroup, my);
+        } else if (ng >= th) {
+            ++n_groups;
+            flat_pass<1>(ng, nc, nact, rank, lane, ws, tbound, tgroup, my);
+        } else if (nn >= th) {
+            n_bounds += 8;
+            flat_pass<2>(nn, ng, nact, rank, lane, ws, tbound, tgroup, my);
+        } else {
+            break;
+        }
+    }
+    h.cand = nc;
+    h.group = ng;
+    h.node = nn;
+}
+
+template <bool kStats>
+__device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
+                                                 const float4* tgroup, WaveScratch* ws,
+                                                 const f3 o, const f3 d, float& max_t, int& best,
+                                                 uint64_t& groups_tested,
+                                                 uint64_t& bounds_tested) {
+    FlatRay my;
+    my.ox = o.x;
+    my.oy = o.y;
+    my.oz = o.z;
+    my.dx = d.x;
+    my.dy = d.y;
+    my.dz = d.z;
+    my.a = dot(d, d);
+    my.br = box_ray(p, o, d);
+    const BoxRay& br = my.br;
+    CullRay r;
+    r.ox = (v2f){o.x, o.x};
+    r.oy = (v2f){o.y, o.y};
+    r.oz = (v2f){o.z, o.z};
+    {
+        const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {my.a, my.a};
+        for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
+            exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, my.a, max_t, best);
+    }
+    uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
+    const uint32_t lane = threadIdx.x & 63u;
+    // finished lanes are masked off for the whole scan: entries go to the live lanes by rank
     const uint64_t live = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(live), rank = lanes_below(live);
-    const uint32_t cnt = (uint32_t)__popcll(need);
-    uint32_t total;
-    const uint32_t pre = wave_prefix(cnt, total);
-    if (total > (uint32_t)kPairCap) return false;
-    {  // list my pairs
-        uint64_t m = need;
-        uint32_t pos = pre;
-        while (m) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            ws->pair[pos++] = (uint16_t)((lane << 6) | k);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint32_t ncand = 0;  // wave-uniform
-    for (uint32_t i0 = 0; i0 < total; i0 += nact) {
-        ++n_passes;
-        const uint32_t i = i0 + rank;
-        const bool act = i < total;
-        const uint32_t pr = act ? (uint32_t)ws->pair[i] : (lane << 6);
-        const int owner = (int)(pr >> 6);
-        // the owner's ray (ds_bpermute; owners are active lanes)
-        const float qx = __shfl(o.x, owner), qy = __shfl(o.y, owner), qz = __shfl(o.z, owner);
-        const float ex = __shfl(d.x, owner), ey = __shfl(d.y, owner), ez = __shfl(d.z, owner);
-        const float qa = __shfl(a, owner);
-        uint32_t hits = 0;
-        v2f hb01, cc01, d01, hb23, cc23, d23;
-        float4 idf = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (act) {
-            const float4* g = tg + __umul24(pr & 63u, 5u);
-            const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
-            const v2f ox = {qx, qx}, oy = {qy, qy}, oz = {qz, qz};
-            const v2f dx = {ex, ex}, dy = {ey, ey}, dz = {ez, ez}, a2 = {qa, qa};
-            pair_disc_cc(ox, oy, oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
-            pair_disc_cc(ox, oy, oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
-            hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
-            hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
-            hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
-            hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
-            if (hits) idf = g[4];
-        }
-        // list the candidates (a full list is resolved first)
-        uint32_t ctot;
-        const uint32_t cpre = wave_prefix((uint32_t)__popc(hits), ctot);
-        if (ncand + ctot > (uint32_t)kCandCap) {
-            __builtin_amdgcn_wave_barrier();
-            resolve_cands(ws, ncand, rank, nact);
-            __builtin_amdgcn_wave_barrier();
-            ncand = 0;
-        }
-        const bool direct = ctot > (uint32_t)kCandCap;  // more than the list holds: in place
-        uint32_t pos = ncand + cpre;
-        const uint32_t ownbits = (uint32_t)owner << 24;
-        while (hits) {
-            const int s = __builtin_ctz(hits);
-            hits &= hits - 1;
-            const float hb = s == 0 ? hb01.x : s == 1 ? hb01.y : s == 2 ? hb23.x : hb23.y;
-            const float ds = s == 0 ? d01.x : s == 1 ? d01.y : s == 2 ? d23.x : d23.y;
-            const float ix = s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w;
-            if (direct) {
-                const float t = candidate_t(hb, ds, qa);
-                if (t > 0.001f && t < 1e5f)
-                    atomicMin(&ws->key[owner], pack_hit(t, (int)__float_as_uint(ix)));
-            } else {
-                ws->cand[pos++] =
-                    make_float4(hb, ds, qa, __uint_as_float(__float_as_uint(ix) | ownbits));
+    ws->key[lane] = pack_hit(max_t, best);
+    FlatStacks h = {0u, 0u, 0u};
+    cfloat4* node = (cfloat4*)p.cnode;
+    cfloat4* top = (cfloat4*)p.ctop;
+    const int ncg = p.ncgroups;
+    uint32_t tops = 0;
+    for (int base = 0;; base += 64) {
+        uint32_t th = 1u;  // past the last chunk: drain everything
+        if (base < ncg) {
+            th = nact;
+            // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
+            if ((base & 127) == 0) {
+                const BoundPair tp = load_bound_pair(top + 4 * (base >> 7));
+                tops = ~push_bound_pair(0u, br, tp.b0, tp.b1, tp.b2, tp.b3) & 3u;
+                n_bounds += 2;
+            }
+            const bool in_chunk = ((tops >> ((base >> 6) & 1)) & 1u) != 0;
+            if (__ballot(in_chunk) == 0) continue;
+            // level 1, wave-uniform: nodes of this chunk, per-lane bits -> node entries
+            const int nn = min(8, (ncg - base) >> 3);
+            cfloat4* nb = node + 4 * (base >> 4);
+            uint32_t out = 0;
+            BoundPair cur = load_bound_pair(nb + 4 * ((nn - 2) >> 1));
+            for (int j = nn - 2; j >= 0; j -= 2) {
+                const BoundPair nxt = load_bound_pair(nb + 4 * ((j >= 2 ? j - 2 : j) >> 1));
+                out = push_bound_pair(out, br, cur.b0, cur.b1, cur.b2, cur.b3);
+                cur = nxt;
+            }
+            n_bounds += (uint32_t)nn;
+            uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
+            uint32_t tot;
+            uint32_t pos = h.node + wave_prefix<4>((uint32_t)__popc(nodes), tot);
+            h.node += tot;
+            if (nodes) {
+                const uint32_t tag = (lane << 10) | ((uint32_t)base >> 3);
+                do {
+                    const uint32_t j = (uint32_t)__builtin_ctz(nodes);
+                    nodes &= nodes - 1;
+                    ws->node[pos++] = (uint16_t)(tag | j);
+                } while (nodes);
             }
         }
-        if (!direct) ncand += ctot;
+        flat_drain(th, nact, rank, lane, ws, h, tbound, tgroup, my, n_groups, n_bounds);
+        if (base >= ncg) break;
     }
     __builtin_amdgcn_wave_barrier();
-    resolve_cands(ws, ncand, rank, nact);
-    __builtin_amdgcn_wave_barrier();
-    return true;
+    const unsigned long long k = ws->key[lane];
+    max_t = __uint_as_float((uint32_t)(k >> 32));
+    best = (int)(uint32_t)k;
+    bounds_tested += __builtin_amdgcn_readfirstlane(n_bounds);
+    groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
 }
 
-template <bool kStats, bool kFlat = false>
+template <bool kStats>
 __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const float4* tbound,
                                                  const float4* tgroup, const f3 o, const f3 d,
                                                  float& max_t, int& best,
                                                  uint64_t& groups_tested,
                                                  uint64_t& bounds_tested, uint32_t& lane_cnt,
-                                                 uint32_t& rounds, WaveScratch* ws = nullptr) {
+                                                 uint32_t& rounds) {
     const float a = dot(d, d);
-    const float inv = __builtin_amdgcn_rsqf(a);
     CullRay r;
     r.ox = (v2f){o.x, o.x};
     r.oy = (v2f){o.y, o.y};
     r.oz = (v2f){o.z, o.z};
-    r.wx = (v2f){d.x * inv, d.x * inv};
-    r.wy = (v2f){d.y * inv, d.y * inv};
-    r.wz = (v2f){d.z * inv, d.z * inv};
+    const BoxRay br = box_ray(p, o, d);
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* top = (cfloat4*)p.ctop;
@@ -596,27 +762,25 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
         exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
     // per-segment pass counters, wave-uniform: kept in SGPRs, folded into the 64-bit totals once
     uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
-    const uint32_t lane = threadIdx.x & 63u;
-    if constexpr (kFlat) ws->key[lane] = pack_hit(max_t, best);
     uint32_t tops = 0;
     for (int base = 0; base < ncg; base += 64) {
         // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
         if ((base & 127) == 0) {
-            const BoundPair tp = load_bound_pair(top + 3 * (base >> 7));
-            tops = ~push_bound_pair(0u, r, tp.b0, tp.b1, tp.b2) & 3u;
+            const BoundPair tp = load_bound_pair(top + 4 * (base >> 7));
+            tops = ~push_bound_pair(0u, br, tp.b0, tp.b1, tp.b2, tp.b3) & 3u;
             n_bounds += 2;
         }
         const bool in_chunk = ((tops >> ((base >> 6) & 1)) & 1u) != 0;
         if (__ballot(in_chunk) == 0) continue;
         // level 1, wave-uniform: nodes of this chunk, per-lane bits
         const int nn = min(8, (ncg - base) >> 3);
-        cfloat4* nb = node + 3 * (base >> 4);
+        cfloat4* nb = node + 4 * (base >> 4);
         // sign bits pushed from the last node down, so bit j ends up = node j ruled out
         uint32_t out = 0;
-        BoundPair cur = load_bound_pair(nb + 3 * ((nn - 2) >> 1));
+        BoundPair cur = load_bound_pair(nb + 4 * ((nn - 2) >> 1));
         for (int j = nn - 2; j >= 0; j -= 2) {
-            const BoundPair nxt = load_bound_pair(nb + 3 * ((j >= 2 ? j - 2 : j) >> 1));
-            out = push_bound_pair(out, r, cur.b0, cur.b1, cur.b2);
+            const BoundPair nxt = load_bound_pair(nb + 4 * ((j >= 2 ? j - 2 : j) >> 1));
+            out = push_bound_pair(out, br, cur.b0, cur.b1, cur.b2, cur.b3);
             cur = nxt;
         }
         uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
@@ -628,25 +792,17 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             if (nodes) {
                 const int j = __builtin_ctz(nodes);
                 nodes &= nodes - 1;
-                const float4* gb = tbound + 3 * (base >> 1) + __umul24((uint32_t)j, 12u);
+                const float4* gb = tbound + 4 * (base >> 1) + __umul24((uint32_t)j, 16u);
                 uint32_t gout = 0;
 #pragma unroll
                 for (int k = 3; k >= 0; k--) {
-                    const float4 b0 = gb[3 * k], b1 = gb[3 * k + 1], b2 = gb[3 * k + 2];
-                    gout = push_bound_pair(gout, r, b0, b1, make_float2(b2.x, b2.y));
+                    gout = push_bound_pair(gout, br, gb[4 * k], gb[4 * k + 1], gb[4 * k + 2],
+                                           gb[4 * k + 3]);
                 }
                 need |= (uint64_t)(~gout & 0xffu) << (8 * j);
             }
         }
         if constexpr (kStats) lane_cnt += (uint32_t)__popcll(need);
-        if constexpr (kFlat) {
-            if (exact_flat(ws, tgroup + 5 * base, need, o, d, a, lane, n_groups)) continue;
-            // too many pairs for the list: the per-lane loop, on registers synced with the key
-            __builtin_amdgcn_wave_barrier();
-            const unsigned long long k = ws->key[lane];
-            max_t = __uint_as_float((uint32_t)(k >> 32));
-            best = (int)(uint32_t)k;
-        }
         // the exact test, per lane on its own groups
         while (__ballot(need != 0)) {
             ++n_groups;
@@ -682,13 +838,6 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
                 rounds += cand;
             }
         }
-        if constexpr (kFlat) ws->key[lane] = pack_hit(max_t, best);
-    }
-    if constexpr (kFlat) {
-        __builtin_amdgcn_wave_barrier();
-        const unsigned long long k = ws->key[lane];
-        max_t = __uint_as_float((uint32_t)(k >> 32));
-        best = (int)(uint32_t)k;
     }
     bounds_tested += __builtin_amdgcn_readfirstlane(n_bounds);
     groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
@@ -727,7 +876,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
     WaveScratch* ws = nullptr;
     if constexpr (kCull == 2 || kCull == 4) {
-        const int nb = (p.ncgroups >> 1) * 3, ng = p.ncgroups * 5;
+        const int nb = (p.ncgroups >> 1) * 4, ng = p.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = p.cbound[i];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = tgroup[i];
         __syncthreads();
@@ -830,8 +979,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kCull == 4)
-                    scan_culled_lane<kStats, true>(p, tbound, tgroup, o, d, max_t, best,
-                                                   w_groups, w_bounds, lane_cnt, hit_groups, ws);
+                    scan_culled_flat<kStats>(p, tbound, tgroup, ws, o, d, max_t, best, w_groups,
+                                             w_bounds);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);

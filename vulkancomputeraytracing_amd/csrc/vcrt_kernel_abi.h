@@ -36,10 +36,12 @@ struct TraceParams {
                             //   (cx0,cx1,cy0,cy1) (cz0,cz1,r0^2,r1^2) (cx2..) (cz2..) + the
                             //   members' world[] indices as int bits (-1 = padding); the nbig
                             //   big-sphere groups first, then the hierarchy in spatial order
-    const float4* cbound;   // [ncgroups / 2 * 3] bounds of group pairs, pair-SoA:
-                            //   (Cx0,Cx1,Cy0,Cy1) (Cz0,Cz1,K0,K1) (Rk0,Rk1,0,0), tracer.hip
-    const float4* cnode;    // [ncgroups / 16 * 3] bounds of node pairs (8 groups per node)
-    const float4* ctop;     // bounds of pairs of 64-group chunks, same form
+    const float4* cbound;   // [ncgroups / 2 * 4] boxes of group pairs, pair-SoA:
+                            //   (lox0,lox1,loy0,loy1) (loz0,loz1,hix0,hix1) (hiy0,hiy1,hiz0,hiz1)
+                            //   (K0,K1,0,0), K = 8.1u / r_min of the box's members
+    const float4* cnode;    // [ncgroups / 16 * 4] boxes of node pairs (8 groups per node)
+    const float4* ctop;     // boxes of pairs of 64-group chunks, same form
+    float box_margin[4];    // max |centre|, r_max^2, max |box coordinate|, 0 (rounded up)
     int32_t ncgroups;       // hierarchy groups, multiple of 16
     int32_t nbig;           // big-sphere groups tested for every ray
     int32_t nspheres;
@@ -54,7 +56,8 @@ struct TraceParams {
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
 };
 
-constexpr uint32_t kWaveScratchBytes = 3584;  // CULL_FLAT per-wave LDS scratch (tracer.hip)
+constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
+constexpr uint32_t kWaveScratchBytes = 4096;  // CULL_FLAT per-wave LDS stacks (tracer.hip WaveScratch)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 constexpr uint32_t kFlagSlab = 4u;          // chunk sums always go to the slab (resolve pass)

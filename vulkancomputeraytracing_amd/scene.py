@@ -64,26 +64,29 @@ def cull_tables(spheres: np.ndarray) -> dict | None:
     """The culled scans' tables for `spheres` (host computation, no GPU): ``nbig`` big-sphere
     groups tested for every ray, then ``G`` hierarchy groups. ``geom`` [nbig + G, 16] pair-SoA
     groups and ``index`` [nbig + G, 4] world[] indices (-1 = padding), big groups first;
-    ``bound`` [G/2, 12] hierarchy group-pair bounds, ``node`` [G/16, 12] node-pair bounds
-    (node i = hierarchy groups 8i..8i+7), ``top`` chunk-pair bounds (entry i = hierarchy
-    groups 64i..64i+63). None when culling does not apply (< 16 spheres, unbounded)."""
+    ``bound`` [G/2, 12] hierarchy group-pair boxes, ``node`` [G/16, 12] node-pair boxes
+    (node i = hierarchy groups 8i..8i+7), ``top`` chunk-pair boxes (entry i = hierarchy
+    groups 64i..64i+63), ``margin`` the box-test constants (max |centre|, r_max^2, max |box
+    coordinate|, 0). None when culling does not apply (< 16 spheres, unbounded)."""
     spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
     lib = N.lib()
     ptr = spheres.ctypes.data
     nbig = ctypes.c_int32(0)
     g = lib.vcrt_cull_tables(ptr, len(spheres), None, None, None, None, None,
-                             ctypes.byref(nbig), 0)
+                             ctypes.byref(nbig), None, 0)
     if g == 0:
         return None
     nb = nbig.value
     geom = np.zeros((nb + g, 16), np.float32)
-    bound = np.zeros((g // 2, 12), np.float32)
-    node = np.zeros((g // 16, 12), np.float32)
+    bound = np.zeros((g // 2, 16), np.float32)
+    node = np.zeros((g // 16, 16), np.float32)
     nt = (g + 63) // 64
-    top = np.zeros(((nt + (nt & 1)) // 2, 12), np.float32)
+    top = np.zeros(((nt + (nt & 1)) // 2, 16), np.float32)
     index = np.zeros((nb + g, 4), np.int32)
+    margin = np.zeros(4, np.float32)
     got = lib.vcrt_cull_tables(ptr, len(spheres), geom.ctypes.data, bound.ctypes.data,
                                node.ctypes.data, top.ctypes.data, index.ctypes.data,
-                               ctypes.byref(nbig), nb + g)
+                               ctypes.byref(nbig), margin.ctypes.data, nb + g)
     assert got == g
-    return {"nbig": nb, "geom": geom, "bound": bound, "node": node, "top": top, "index": index}
+    return {"nbig": nb, "geom": geom, "bound": bound, "node": node, "top": top, "index": index,
+            "margin": margin}
