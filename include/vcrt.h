@@ -121,8 +121,11 @@ typedef struct vcrt_stats {
     uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
     uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
     uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */
-    uint64_t debug[8]; /* diagnostics (VCRT_DEBUG_STATS=1): wave-iterations, active-lane sum,
-                          hit groups, fetches, last/first wave end time, sum end time, waves */
+    uint64_t debug[24]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
+                           active-lane sum, hit groups, fetches, last/first wave end time, sum
+                           end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,
+                           its uniform levels, node / group / candidate passes (CULL_FLAT),
+                           candidate passes run, the whole wave, the big list, node pushes */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

@@ -1,0 +1,20 @@
+# Where the flat scan's wave time goes (VCRT_DEBUG_STATS=1: s_memtime per phase, stats kernel),
+# final scene 1080p 64 spp; variant $PV (default 5).
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+VCRT_DEBUG_STATS=1 timeout -k 10 200 python tools/render_once.py --spp 64 --variant ${PV:-5} > gpurun_out/phases.json || exit 1
+python - <<'PY'
+import json
+st = json.load(open("gpurun_out/phases.json"))
+d = st["debug"]
+wi = d[0]
+tot = d[14]
+print("kernel_ms %.2f wave-iters %d waves %d" % (st["kernel_ms"], wi, d[7]))
+for name, k in (("scan", 8), ("big list", 15), ("levels", 9), ("node pushes", 16),
+                ("node passes", 10), ("group passes", 11), ("cand passes", 12)):
+    print("%-13s %5.1f%% of wave time, %8.1f ticks per wave-iter" % (name, 100 * d[k] / tot, d[k] / wi))
+print("cand passes per wave-iter %.2f; node %.2f group %.2f (from counters)" % (
+    d[13] / wi, (st["bound_tests"] / wi), st["group_tests"] / wi))
+print("total ticks per wave-iter %.1f" % (tot / wi))
+PY

@@ -98,7 +98,7 @@ class vcrt_stats(ctypes.Structure):
         ("accumulated_spp", ctypes.c_uint64),
         ("group_tests", ctypes.c_uint64),
         ("bound_tests", ctypes.c_uint64),
-        ("debug", ctypes.c_uint64 * 8),
+        ("debug", ctypes.c_uint64 * 24),
     ]
 
 

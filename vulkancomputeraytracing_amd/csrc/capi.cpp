@@ -381,7 +381,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     g.work_flags |= vcrt::kFlagReverseOrder;
     if (const char* e = std::getenv("VCRT_WORK_ORDER"))
         if (std::strcmp(e, "forward") == 0) g.work_flags &= ~vcrt::kFlagReverseOrder;
-    if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, 64))) != VK_SUCCESS) return fail(r);
+    if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, 192))) != VK_SUCCESS) return fail(r);
 
     // The reference's world[] is compiled in; default to the same final scene.
     std::vector<vcrt_sphere> world;
@@ -612,7 +612,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
         VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
         if (g.debug_stats) {
-            unsigned long long init[8] = {0, 0, 0, 0, 0, ~0ull, 0, 0};
+            unsigned long long init[24] = {0, 0, 0, 0, 0, ~0ull};
             VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
                                     g.stream));
         }

@@ -630,25 +630,43 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
 }
 
 // Runs passes while a stack holds at least `th` entries (th = nact: full passes only; 1: drain).
+// Stats builds: wave clock ticks per phase (s_memtime, wave-uniform).
+struct PhaseTicks {
+    uint64_t scan = 0, levels = 0, node = 0, group = 0, cand = 0, cand_passes = 0, big = 0,
+             push = 0;
+};
+
+__device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
+
 struct FlatStacks {  // wave-uniform stack heights
     uint32_t cand, group, node;
 };
 
+template <bool kStats>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
                                            WaveScratch* ws, FlatStacks& h, const float4* tbound,
                                            const float4* tgroup, const FlatRay& my,
-                                           uint32_t& n_groups, uint32_t& n_bounds) {
+                                           uint32_t& n_groups, uint32_t& n_bounds,
+                                           PhaseTicks& pt) {
     uint32_t nc = h.cand, ng = h.group, nn = h.node;
     for (;;) {
         __builtin_amdgcn_wave_barrier();  // the entries were written by other lanes
+        uint64_t t0 = 0;
+        if constexpr (kStats) t0 = ticks();
         if (nc >= th) {
             flat_pass<0>(nc, nc, nact, rank, lane, ws, tbound, tgroup, my);
+            if constexpr (kStats) {
+                pt.cand += ticks() - t0;
+                ++pt.cand_passes;
+            }
         } else if (ng >= th) {
             ++n_groups;
             flat_pass<1>(ng, nc, nact, rank, lane, ws, tbound, tgroup, my);
+            if constexpr (kStats) pt.group += ticks() - t0;
         } else if (nn >= th) {
             n_bounds += 8;
             flat_pass<2>(nn, ng, nact, rank, lane, ws, tbound, tgroup, my);
+            if constexpr (kStats) pt.node += ticks() - t0;
         } else {
             break;
         }
@@ -662,8 +680,10 @@ template <bool kStats>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
                                                  const float4* tgroup, WaveScratch* ws,
                                                  const f3 o, const f3 d, float& max_t, int& best,
-                                                 uint64_t& groups_tested,
-                                                 uint64_t& bounds_tested) {
+                                                 uint64_t& groups_tested, uint64_t& bounds_tested,
+                                                 PhaseTicks& pt) {
+    uint64_t t_in = 0;
+    if constexpr (kStats) t_in = ticks();
     FlatRay my;
     my.ox = o.x;
     my.oy = o.y;
@@ -683,6 +703,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
         for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
             exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, my.a, max_t, best);
     }
+    if constexpr (kStats) pt.big += ticks() - t_in;
     uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
     const uint32_t lane = threadIdx.x & 63u;
     // finished lanes are masked off for the whole scan: entries go to the live lanes by rank
@@ -698,6 +719,8 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
         uint32_t th = 1u;  // past the last chunk: drain everything
         if (base < ncg) {
             th = nact;
+            uint64_t t0 = 0;
+            if constexpr (kStats) t0 = ticks();
             // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
             if ((base & 127) == 0) {
                 const BoundPair tp = load_bound_pair(top + 4 * (base >> 7));
@@ -718,6 +741,11 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             }
             n_bounds += (uint32_t)nn;
             uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
+            if constexpr (kStats) {
+                const uint64_t t1 = ticks();
+                pt.levels += t1 - t0;
+                t0 = t1;
+            }
             uint32_t tot;
             uint32_t pos = h.node + wave_prefix<4>((uint32_t)__popc(nodes), tot);
             h.node += tot;
@@ -729,8 +757,10 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                     ws->node[pos++] = (uint16_t)(tag | j);
                 } while (nodes);
             }
+            if constexpr (kStats) pt.push += ticks() - t0;
         }
-        flat_drain(th, nact, rank, lane, ws, h, tbound, tgroup, my, n_groups, n_bounds);
+        flat_drain<kStats>(th, nact, rank, lane, ws, h, tbound, tgroup, my, n_groups, n_bounds,
+                           pt);
         if (base >= ncg) break;
     }
     __builtin_amdgcn_wave_barrier();
@@ -901,6 +931,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     unsigned long long segs = 0;
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
     uint64_t w_groups = 0, w_bounds = 0;  // per wave (uniform): sphere groups / bounds tested
+    PhaseTicks pt;                         // stats builds: wave clock per phase
+    uint64_t t_begin = 0;
+    if constexpr (kStats) t_begin = ticks();
     // the wave's current block of items (wave-uniform); 64 = exhausted, fetch a new one
     const uint32_t total_blocks = p.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
@@ -975,15 +1008,18 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(!guarded) == 0) {
                 uint32_t lane_cnt = 0;
+                uint64_t t0 = 0;
+                if constexpr (kStats) t0 = ticks();
                 if constexpr (kCull == 1)
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kCull == 4)
                     scan_culled_flat<kStats>(p, tbound, tgroup, ws, o, d, max_t, best, w_groups,
-                                             w_bounds);
+                                             w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);
+                if constexpr (kStats) pt.scan += ticks() - t0;
                 if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
                     for (int off = 32; off > 0; off >>= 1)
                         lane_cnt = max(lane_cnt, (uint32_t)__shfl_xor((int)lane_cnt, off));
@@ -1103,6 +1139,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             atomicMin(p.debug + 5, t);
             atomicAdd(p.debug + 6, t >> 8);  // mean wave end time (in 256-tick units)
             atomicAdd(p.debug + 7, 1ull);
+            atomicAdd(p.debug + 8, (unsigned long long)pt.scan);
+            atomicAdd(p.debug + 9, (unsigned long long)pt.levels);
+            atomicAdd(p.debug + 10, (unsigned long long)pt.node);
+            atomicAdd(p.debug + 11, (unsigned long long)pt.group);
+            atomicAdd(p.debug + 12, (unsigned long long)pt.cand);
+            atomicAdd(p.debug + 13, (unsigned long long)pt.cand_passes);
+            atomicAdd(p.debug + 14, (unsigned long long)(ticks() - t_begin));
+            atomicAdd(p.debug + 15, (unsigned long long)pt.big);
+            atomicAdd(p.debug + 16, (unsigned long long)pt.push);
         }
     }
 }
@@ -1141,7 +1186,11 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats
 
 // Per-lane scan with the exact phase flattened over the wave (exact_flat): LDS tables plus
 // 3.5 KB of scratch per wave.
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void vcrt_trace_cull_flat(TraceParams p) {
+#ifndef VCRT_FLAT_WAVES
+#define VCRT_FLAT_WAVES 5  // waves per SIMD the flat scan is compiled for (LDS allows 5)
+#endif
+extern "C" __global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, false, 4>(p, lds_tab);
 }
