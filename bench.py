@@ -61,7 +61,8 @@ def cpu_baseline(args):
     threads = min(16, os.cpu_count() or 1)
     scene = o.scene(args.scene)
     # calibrate on a tiny sample, then size the real one for ~cpu_seconds of work
-    probe_rows, probe_spp = range(0, args.height, max(1, args.height // 8)), 2
+    # (34 rows spread over the frame: sky, spheres and ground in frame proportion)
+    probe_rows, probe_spp = range(0, args.height, max(1, args.height // 32)), 2
     t0 = time.perf_counter()
     o.render(o.config(args.width, args.height, probe_spp, args.depth), scene, rows=probe_rows,
              threads=threads)

@@ -125,7 +125,8 @@ typedef struct vcrt_stats {
                            active-lane sum, hit groups, fetches, last/first wave end time, sum
                            end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,
                            its uniform levels, node / group / candidate passes (CULL_FLAT),
-                           candidate passes run, the whole wave, the big list, node pushes */
+                           candidate passes run, the whole wave, the big list, node pushes,
+                           [17..18] shading and sky, block fetch */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

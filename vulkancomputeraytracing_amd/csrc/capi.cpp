@@ -52,7 +52,7 @@ struct RendererState {
                   k_trace_cull_lane_lds_wide_stats = nullptr, k_trace_cull_flat = nullptr,
                   k_trace_cull_flat_stats = nullptr;
     int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
-    // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=reverse)
+    // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     bool debug_stats = false;
     uint32_t work_flags = 0;
     void* d_debug = nullptr;

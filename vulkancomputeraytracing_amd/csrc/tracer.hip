@@ -331,13 +331,15 @@ __device__ __forceinline__ uint32_t bound_pair_need(const BoxRay& r, const Bound
 __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay& r, v2f dx, v2f dy,
                                                     v2f dz, v2f a2, float a, float& max_t,
                                                     int& best) {
-    const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
-    v2f hb01, cc01, d01, hb23, cc23, d23;
+    const float4 q0 = rec[0], q1 = rec[1], idf = rec[4];
+    v2f hb01, cc01, d01, hb23 = {0.f, 0.f}, cc23 = {0.f, 0.f}, d23 = {-1.f, -1.f};
     pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
-    pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+    // members 2 and 3 only when the group has them (wave-uniform; the big list of the final
+    // scene is the ground alone)
+    if (__float_as_int(idf.z) >= 0 || __float_as_int(idf.w) >= 0)
+        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, rec[2], rec[3], hb23, cc23, d23);
     const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
     if (__ballot(!(m4 < 0.0f))) {
-        const float4 idf = rec[4];
         if (may_hit(hb01.x, cc01.x, d01.x))
             consider(candidate_t(hb01.x, d01.x, a), __float_as_int(idf.x), max_t, best);
         if (may_hit(hb01.y, cc01.y, d01.y))
@@ -633,7 +635,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
 // Stats builds: wave clock ticks per phase (s_memtime, wave-uniform).
 struct PhaseTicks {
     uint64_t scan = 0, levels = 0, node = 0, group = 0, cand = 0, cand_passes = 0, big = 0,
-             push = 0;
+             push = 0, shade = 0, fetch = 0;
 };
 
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
@@ -941,6 +943,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     for (;;) {
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
+        uint64_t t_fetch = 0;
+        if constexpr (kStats) t_fetch = ticks();
         uint64_t need_mask = __ballot(need && !done);
         while (need_mask) {
             if (blk_next >= 64u) {
@@ -987,6 +991,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             blk_next += min((uint32_t)__popcll(need_mask), avail);
             need_mask = __ballot(need && !done);
         }
+        if constexpr (kStats) pt.fetch += ticks() - t_fetch;
         const uint64_t live = __ballot(!done);
         if (live == 0) break;
         if constexpr (kStats) {
@@ -1036,6 +1041,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         if constexpr (kStats) st_hitgroups += hit_groups;
 
         // ---- shade (textures.glsl) or sky (functions.glsl:85-89) ----
+        uint64_t t_shade = 0;
+        if constexpr (kStats) t_shade = ticks();
         bool ended = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
         if (best >= 0) {
@@ -1117,6 +1124,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                 pass = 0;
             }
         }
+        if constexpr (kStats) pt.shade += ticks() - t_shade;
     }
 
     // one segment-counter atomic per wave
@@ -1148,6 +1156,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             atomicAdd(p.debug + 14, (unsigned long long)(ticks() - t_begin));
             atomicAdd(p.debug + 15, (unsigned long long)pt.big);
             atomicAdd(p.debug + 16, (unsigned long long)pt.push);
+            atomicAdd(p.debug + 17, (unsigned long long)pt.shade);
+            atomicAdd(p.debug + 18, (unsigned long long)pt.fetch);
         }
     }
 }
