@@ -196,8 +196,10 @@ def main():
             executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
                         + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
         kernel = KERNEL_NAMES.get(st["kernel_variant"], "?")
-        if st["kernel_variant"] == 4 and st["lds_bytes"] > 0:
+        if st["kernel_variant"] == 4 and st["tables_in_lds"]:
             kernel += "_lds_wide" if st["block_threads"] == 1024 else "_lds"
+        if st["kernel_variant"] == 5 and not st["tables_in_lds"]:
+            kernel += "_global"
         achieved = executed / (k_ms * 1e-3) / 1e12
         equivalent = flops / (k_ms * 1e-3) / 1e12
         traffic = None

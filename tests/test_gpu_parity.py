@@ -134,11 +134,20 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
     assert_bitwise(got, want, f"{scene} lane tables={tables}")
     assert st["segments"] == segs
     if tables == "global":
-        assert st["lds_bytes"] == 0
-    elif scene == "final":  # 13 KB of tables: 256-thread workgroups, one copy each
+        assert st["lds_bytes"] == 0 and not st["tables_in_lds"]
+    elif scene == "final":  # 14 KB of tables: 256-thread workgroups, one copy each
         assert 0 < st["lds_bytes"] <= 32768 and st["block_threads"] == 256
-    elif st["lds_bytes"] > 0:  # 108 KB: one copy per 1024-thread workgroup
+        assert st["tables_in_lds"]
+    elif st["lds_bytes"] > 0:  # 114 KB: one copy per 1024-thread workgroup
         assert st["lds_bytes"] > 32768 and st["block_threads"] == 1024
+    # the flat scan: tables beside its stacks in LDS up to 32 KB, else in global memory
+    got, st = gpu_render(scene, w, h, spp, depth, vc.KERNEL_CULL_FLAT)
+    assert st["kernel_variant"] == vc.KERNEL_CULL_FLAT
+    assert_bitwise(got, want, f"{scene} flat tables={tables}")
+    assert st["segments"] == segs
+    assert st["tables_in_lds"] == (tables == "lds" and scene == "final")
+    if not st["tables_in_lds"]:
+        assert st["lds_bytes"] == 4 * 6400 and st["block_threads"] == 256
 
 
 def culling_torture_scene():
@@ -191,9 +200,9 @@ def test_large_random_scene_all_variants(oracle, n):
         with vc.Renderer(desc, sc) as r:
             r.draw_next_frame()
             got, st = r.read_framebuffer(), r.stats()
-        # CULL_FLAT needs its tables in LDS: these scenes fall back to CULL_LANE
-        want_v = vc.KERNEL_CULL_LANE if variant == vc.KERNEL_CULL_FLAT else variant
-        assert st["kernel_variant"] == want_v and st["nspheres"] == n
+        assert st["kernel_variant"] == variant and st["nspheres"] == n
+        if variant == vc.KERNEL_CULL_FLAT:  # tables beyond LDS: the global-table flat kernel
+            assert not st["tables_in_lds"]
         assert_bitwise(got, want, f"random {n} v{variant}")
         assert st["segments"] == segs
 

@@ -95,6 +95,7 @@ class vcrt_stats(ctypes.Structure):
         ("nspheres", ctypes.c_int32),
         ("lds_bytes", ctypes.c_uint32),
         ("accumulate_chunk", ctypes.c_int32),
+        ("tables_in_lds", ctypes.c_int32),
         ("accumulated_spp", ctypes.c_uint64),
         ("group_tests", ctypes.c_uint64),
         ("bound_tests", ctypes.c_uint64),

@@ -50,7 +50,8 @@ struct RendererState {
                   k_trace_cull_lane_lds_stats = nullptr, k_trace_cull_lane = nullptr,
                   k_trace_cull_lane_stats = nullptr, k_trace_cull_lane_lds_wide = nullptr,
                   k_trace_cull_lane_lds_wide_stats = nullptr, k_trace_cull_flat = nullptr,
-                  k_trace_cull_flat_stats = nullptr;
+                  k_trace_cull_flat_stats = nullptr, k_trace_cull_flat_global = nullptr,
+                  k_trace_cull_flat_global_stats = nullptr;
     int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     bool debug_stats = false;
@@ -199,6 +200,9 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_stats, m, "vcrt_trace_cull_lane_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat, m, "vcrt_trace_cull_flat"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_stats, m, "vcrt_trace_cull_flat_stats"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_global, m, "vcrt_trace_cull_flat_global"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_global_stats, m,
+                                  "vcrt_trace_cull_flat_global_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide, m,
                                   "vcrt_trace_cull_lane_lds_wide"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide_stats, m,
@@ -569,11 +573,10 @@ vcrt_result vcrt_draw_next_frame(void) {
              variant == VCRT_KERNEL_CULL_FLAT) &&
             g.ncgroups == 0)
             variant = VCRT_KERNEL_SMEM;
-        // the flattened exact phase needs its tables in LDS beside 3.5 KB of scratch per wave
-        constexpr uint32_t kFlatScratch = 4 * vcrt::kWaveScratchBytes;  // 4 waves per block
-        if (variant == VCRT_KERNEL_CULL_FLAT &&
-            (!lane_lds || lane_wide || g.ncgroups > vcrt::kFlatMaxGroups))
-            variant = VCRT_KERNEL_CULL_LANE;
+        // the flat scan keeps 4 KB of stacks per wave in LDS (4 waves per block), beside its
+        // tables when they fit in 32 KB (16-bit entries); otherwise the tables stay in global
+        // memory and the stacks take 32-bit entries (6.25 KB per wave)
+        const bool flat_lds = lane_lds && !lane_wide && g.ncgroups <= vcrt::kFlatMaxGroups;
         hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
         uint32_t lds = 0;
         if (variant == VCRT_KERNEL_LDS) {
@@ -583,10 +586,14 @@ vcrt_result vcrt_draw_next_frame(void) {
         } else if (variant == VCRT_KERNEL_CULL) {
             f = g.k_trace_cull;
             fs = g.k_trace_cull_stats;
-        } else if (variant == VCRT_KERNEL_CULL_FLAT) {
+        } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_lds) {
             f = g.k_trace_cull_flat;
             fs = g.k_trace_cull_flat_stats;
-            lds = tab_lds + kFlatScratch;
+            lds = tab_lds + 4 * vcrt::kWaveScratchBytes;
+        } else if (variant == VCRT_KERNEL_CULL_FLAT) {
+            f = g.k_trace_cull_flat_global;
+            fs = g.k_trace_cull_flat_global_stats;
+            lds = 4 * vcrt::kWaveScratchBytesWide;
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
             f = g.k_trace_cull_lane_lds_wide;
             fs = g.k_trace_cull_lane_lds_wide_stats;
@@ -652,6 +659,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         g.stats.block_threads = static_cast<int32_t>(block);
         g.stats.kernel_variant = variant;
         g.stats.lds_bytes = lds;
+        g.stats.tables_in_lds = (f == g.k_trace_cull_flat || f == g.k_trace_cull_lane_lds ||
+                                 f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
     }
     VCRT_TRY(hipStreamSynchronize(g.stream));
     g.stats.sphere_tests = g.stats.segments * static_cast<uint64_t>(g.nspheres);

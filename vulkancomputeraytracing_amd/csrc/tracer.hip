@@ -27,6 +27,8 @@
 //     accumulation order. No MFMA.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "vcrt_kernel_abi.h"
 #include "vcrt_math.h"
 
@@ -496,13 +498,26 @@ constexpr int kNodeCap = 576;
 constexpr int kGroupCap = 576;
 constexpr int kCandCap = 320;
 
-struct WaveScratch {
-    unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
-    uint32_t cand[kCandCap];     // owner << 12 | group << 2 | member
-    uint16_t group[kGroupCap];   // owner << 10 | group
-    uint16_t node[kNodeCap];     // owner << 10 | node
+// Stack entries: narrow (16-bit, owner << 10 | index, up to 1024 groups: the LDS-table
+// kernel) or wide (32-bit, owner << 24 | index: the global-table kernel for large scenes).
+// Candidate entries are 32-bit either way: (node/group entry) << 2 | member.
+template <bool kWide>
+struct FlatFmt {
+    using entry_t = typename std::conditional<kWide, uint32_t, uint16_t>::type;
+    static constexpr int kShift = kWide ? 24 : 10;  // owner field of node / group entries
+    static constexpr uint32_t kMask = (1u << kShift) - 1u;
 };
-static_assert(sizeof(WaveScratch) == kWaveScratchBytes, "host LDS size");
+
+template <bool kWide>
+struct WaveScratch {
+    using entry_t = typename FlatFmt<kWide>::entry_t;
+    unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
+    uint32_t cand[kCandCap];     // group entry << 2 | member
+    entry_t group[kGroupCap];    // owner << kShift | group
+    entry_t node[kNodeCap];      // owner << kShift | node
+};
+static_assert(sizeof(WaveScratch<false>) == kWaveScratchBytes, "host LDS size");
+static_assert(sizeof(WaveScratch<true>) == kWaveScratchBytesWide, "host LDS size");
 
 __device__ __forceinline__ unsigned long long pack_hit(float t, int idx) {
     return ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)idx;
@@ -537,17 +552,19 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 // 1: group, 2: node. Lanes ranked past the entries run on their own ray and push nothing.
 // kKind 0: cand, 1: group, 2: node. n: this stack's height; pushed: the height of the stack
 // this pass pushes onto (group for node passes, cand for group passes).
-template <int kKind>
+template <int kKind, bool kWide>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
-                                          uint32_t rank, uint32_t lane, WaveScratch* ws,
+                                          uint32_t rank, uint32_t lane, WaveScratch<kWide>* ws,
                                           const float4* tbound, const float4* tgroup,
                                           const FlatRay& my) {
+    using F = FlatFmt<kWide>;
+    using entry_t = typename F::entry_t;
     const uint32_t m = min(n, nact), top = n - m;
     n = top;
     const bool act = rank < m;
     if constexpr (kKind == 2) {  // node: the 8 group bounds of (owner, node)
-        const uint32_t e = act ? (uint32_t)ws->node[top + rank] : (lane << 10);
-        const int src = (int)(e >> 10) << 2;
+        const uint32_t e = act ? (uint32_t)ws->node[top + rank] : (lane << F::kShift);
+        const int src = (int)(e >> F::kShift) << 2;
         BoxRay r;
         const float ix = from_lane(src, my.br.ix.x), iy = from_lane(src, my.br.iy.x),
                     iz = from_lane(src, my.br.iz.x);
@@ -562,7 +579,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         r.cz = (v2f){cz, cz};
         r.c1 = (v2f){c1, c1};
         r.c2 = (v2f){c2, c2};
-        const float4* gb = tbound + __umul24(e & 1023u, 16u);
+        const float4* gb = tbound + 16u * (e & F::kMask);
         uint32_t gout = 0;
 #pragma unroll
         for (int k = 3; k >= 0; k--)
@@ -572,20 +589,20 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         uint32_t pos = pushed + wave_prefix<4>((uint32_t)__popc(need), tot);
         pushed += tot;
         if (need) {
-            const uint32_t tag = (e & ~1023u) | ((e & 1023u) << 3);
+            const uint32_t tag = (e & ~F::kMask) | ((e & F::kMask) << 3);
             do {
                 const uint32_t k = (uint32_t)__builtin_ctz(need);
                 need &= need - 1;
-                ws->group[pos++] = (uint16_t)(tag | k);
+                ws->group[pos++] = (entry_t)(tag | k);
             } while (need);
         }
     } else if constexpr (kKind == 1) {  // group: exact test of the 4 members for the owner's ray
-        const uint32_t e = act ? (uint32_t)ws->group[top + rank] : (lane << 10);
-        const int src = (int)(e >> 10) << 2;
+        const uint32_t e = act ? (uint32_t)ws->group[top + rank] : (lane << F::kShift);
+        const int src = (int)(e >> F::kShift) << 2;
         const float ox = from_lane(src, my.ox), oy = from_lane(src, my.oy), oz = from_lane(src, my.oz);
         const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
         const float a = from_lane(src, my.a);
-        const float4* g = tgroup + __umul24(e & 1023u, 5u);
+        const float4* g = tgroup + 5u * (e & F::kMask);
         const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
         const v2f vox = {ox, ox}, voy = {oy, oy}, voz = {oz, oz};
         const v2f vdx = {dx, dx}, vdy = {dy, dy}, vdz = {dz, dz}, a2 = {a, a};
@@ -609,13 +626,13 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
             } while (hits);
         }
     } else {  // cand: the member's root (its hb, cc, disc recomputed as the packed test did)
-        const uint32_t e = act ? ws->cand[top + rank] : (lane << 12);
-        const int src = (int)(e >> 12) << 2;
+        const uint32_t e = act ? ws->cand[top + rank] : (lane << (F::kShift + 2));
+        const int src = (int)(e >> (F::kShift + 2)) << 2;
         const float ox = from_lane(src, my.ox), oy = from_lane(src, my.oy), oz = from_lane(src, my.oz);
         const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
         const float a = from_lane(src, my.a);
         const uint32_t s = e & 3u;
-        const float4* g = tgroup + __umul24((e >> 2) & 1023u, 5u);
+        const float4* g = tgroup + 5u * ((e >> 2) & F::kMask);
         const float4 xy = g[(s >> 1) * 2], zr = g[(s >> 1) * 2 + 1], idf = g[4];
         const bool hi = (s & 1u) != 0;
         const float cx = hi ? xy.y : xy.x, cy = hi ? xy.w : xy.z;
@@ -627,7 +644,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const float t = candidate_t(hb, disc, a);
         const float ix = s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w;
         if (act && t > 0.001f && t < 1e5f)
-            atomicMin(&ws->key[e >> 12], pack_hit(t, __float_as_int(ix)));
+            atomicMin(&ws->key[e >> (F::kShift + 2)], pack_hit(t, __float_as_int(ix)));
     }
 }
 
@@ -644,9 +661,10 @@ struct FlatStacks {  // wave-uniform stack heights
     uint32_t cand, group, node;
 };
 
-template <bool kStats>
+template <bool kStats, bool kWide>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
-                                           WaveScratch* ws, FlatStacks& h, const float4* tbound,
+                                           WaveScratch<kWide>* ws, FlatStacks& h,
+                                           const float4* tbound,
                                            const float4* tgroup, const FlatRay& my,
                                            uint32_t& n_groups, uint32_t& n_bounds,
                                            PhaseTicks& pt) {
@@ -656,18 +674,18 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         uint64_t t0 = 0;
         if constexpr (kStats) t0 = ticks();
         if (nc >= th) {
-            flat_pass<0>(nc, nc, nact, rank, lane, ws, tbound, tgroup, my);
+            flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tgroup, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (ng >= th) {
             ++n_groups;
-            flat_pass<1>(ng, nc, nact, rank, lane, ws, tbound, tgroup, my);
+            flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tgroup, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (nn >= th) {
             n_bounds += 8;
-            flat_pass<2>(nn, ng, nact, rank, lane, ws, tbound, tgroup, my);
+            flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tgroup, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else {
             break;
@@ -678,9 +696,9 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
     h.node = nn;
 }
 
-template <bool kStats>
+template <bool kStats, bool kWide>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
-                                                 const float4* tgroup, WaveScratch* ws,
+                                                 const float4* tgroup, WaveScratch<kWide>* ws,
                                                  const f3 o, const f3 d, float& max_t, int& best,
                                                  uint64_t& groups_tested, uint64_t& bounds_tested,
                                                  PhaseTicks& pt) {
@@ -752,16 +770,17 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             uint32_t pos = h.node + wave_prefix<4>((uint32_t)__popc(nodes), tot);
             h.node += tot;
             if (nodes) {
-                const uint32_t tag = (lane << 10) | ((uint32_t)base >> 3);
+                const uint32_t tag = (lane << FlatFmt<kWide>::kShift) | ((uint32_t)base >> 3);
                 do {
                     const uint32_t j = (uint32_t)__builtin_ctz(nodes);
                     nodes &= nodes - 1;
-                    ws->node[pos++] = (uint16_t)(tag | j);
+                    ws->node[pos++] = (typename FlatFmt<kWide>::entry_t)(tag | j);
                 } while (nodes);
             }
             if constexpr (kStats) pt.push += ticks() - t0;
         }
-        flat_drain<kStats>(th, nact, rank, lane, ws, h, tbound, tgroup, my, n_groups, n_bounds,
+        flat_drain<kStats, kWide>(th, nact, rank, lane, ws, h, tbound, tgroup, my, n_groups,
+                                  n_bounds,
                            pt);
         if (base >= ncg) break;
     }
@@ -906,7 +925,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     }
     const float4* tbound = p.cbound;
     const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
-    WaveScratch* ws = nullptr;
+    // the flat scan's stacks: after the LDS tables (kCull 4), or alone with the tables in
+    // global memory and 32-bit entries (kCull 5)
+    constexpr bool kWide = kCull == 5;
+    WaveScratch<kWide>* ws = nullptr;
     if constexpr (kCull == 2 || kCull == 4) {
         const int nb = (p.ncgroups >> 1) * 4, ng = p.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = p.cbound[i];
@@ -915,8 +937,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         tbound = lds_geom;
         tgroup = lds_geom + nb;
         if constexpr (kCull == 4)
-            ws = reinterpret_cast<WaveScratch*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
+            ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
     }
+    if constexpr (kCull == 5) ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const f3 p00 = mk(p.cam[0], p.cam[1], p.cam[2]);
     const f3 du = mk(p.cam[3], p.cam[4], p.cam[5]);
@@ -1018,8 +1041,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                 if constexpr (kCull == 1)
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
-                else if constexpr (kCull == 4)
-                    scan_culled_flat<kStats>(p, tbound, tgroup, ws, o, d, max_t, best, w_groups,
+                else if constexpr (kCull == 4 || kCull == 5)
+                    scan_culled_flat<kStats, kWide>(p, tbound, tgroup, ws, o, d, max_t, best, w_groups,
                                              w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
@@ -1208,6 +1231,19 @@ __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_stats(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, true, 4>(p, lds_tab);
+}
+
+// The flat scan for tables too large for LDS beside its stacks (the stress scene): tables in
+// global memory (L2-resident), 32-bit stack entries (any group count), stacks alone in LDS.
+extern "C" __global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_global(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 5>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_global_stats(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, true, 5>(p, lds_tab);
 }
 
 // The same with 1024-thread workgroups: one table copy serves 16 waves, so tables of up to

@@ -57,7 +57,8 @@ struct TraceParams {
 };
 
 constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
-constexpr uint32_t kWaveScratchBytes = 4096;  // CULL_FLAT per-wave LDS stacks (tracer.hip WaveScratch)
+constexpr uint32_t kWaveScratchBytes = 4096;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
+constexpr uint32_t kWaveScratchBytesWide = 6400;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 constexpr uint32_t kFlagSlab = 4u;          // chunk sums always go to the slab (resolve pass)
