@@ -76,6 +76,48 @@ def group_culled(t, o, d, key="bound", rng=None):
     return gap < 0
 
 
+def group_gap(t, o, d, key="bound", near_far=False):
+    """[rays, boxes] fp32 box gaps: box_gap's per-axis min / max (near_far False) or the
+    flat kernel's planes chosen by the sign of 1/d' (push_bound_pair_nf, near_far True)."""
+    b = t[key]
+    G = 2 * b.shape[0]
+    cols = lambda k: np.stack([b[:, k], b[:, k + 1]], 1).reshape(G)  # noqa: E731
+    lo = [cols(0), cols(2), cols(4)]
+    hi = [cols(6), cols(8), cols(10)]
+    K = cols(12)
+    inv, c, c1, c2 = box_ray(t, o, d)
+    tn = tf = None
+    for k in range(3):
+        tl = fma(lo[k][None, :], inv[:, k, None], c[:, k, None])
+        th = fma(hi[k][None, :], inv[:, k, None], c[:, k, None])
+        if near_far:
+            neg = np.signbit(inv[:, k, None])
+            near, far = np.where(neg, th, tl), np.where(neg, tl, th)
+        else:
+            near, far = np.minimum(tl, th), np.maximum(tl, th)
+        tn = near if tn is None else np.maximum(tn, near)
+        tf = far if tf is None else np.minimum(tf, far)
+    with np.errstate(over="ignore", invalid="ignore"):
+        return fma(np.broadcast_to(K[None, :], tn.shape), np.broadcast_to(c2[:, None], tn.shape),
+                   rn(rn(tf - tn) + c1[:, None]))
+
+
+@pytest.mark.parametrize("name", ["final", "stress4096"])
+def test_near_far_planes_equal_min_max(name):
+    """The flat kernel's node passes read each axis' near and far plane by the sign of 1/d'
+    (cbound_nf layout) instead of taking min / max: the gaps, sign bits included, are equal."""
+    rng = np.random.default_rng(11)
+    t = S.cull_tables(S.builtin_scene(name))
+    o, d = random_rays(3000, rng, -20.0, 20.0)
+    d[:100, 0] = 0.0   # zero and negative-zero directions: d' = +-2^-40
+    d[100:200, 1] = -0.0
+    o[200:300] = 0.0
+    a = group_gap(t, o, d, near_far=False)
+    b = group_gap(t, o, d, near_far=True)
+    assert np.array_equal(np.signbit(a), np.signbit(b))
+    assert np.array_equal(a, b)
+
+
 def member_disc(t, o, d):
     """[rays, hierarchy groups, 4] fp32 discriminants exactly as pair_disc computes them."""
     g = t["geom"][t["nbig"]:]

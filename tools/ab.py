@@ -1,0 +1,58 @@
+"""A/B timing of tracer code objects on one configuration: each code object renders the same
+frames in turn (interleaved rounds), and the images must be bit-identical to the first one's.
+
+  python tools/ab.py exp/base.hsaco exp/new.hsaco [--spp 256] [--rounds 2] [--scene final]
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import vulkancomputeraytracing_amd as vc  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("objects", nargs="+")
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--depth", type=int, default=10)
+    p.add_argument("--scene", default="final")
+    p.add_argument("--variant", type=int, default=0)
+    p.add_argument("--frames", type=int, default=2)
+    p.add_argument("--rounds", type=int, default=2)
+    a = p.parse_args()
+    best = {o: None for o in a.objects}
+    digest = {}
+    for rnd in range(a.rounds):
+        for obj in a.objects:
+            desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
+                                 max_depth=a.depth, kernel_variant=a.variant, device=0,
+                                 code_object_path=obj)
+            with vc.Renderer(desc, a.scene) as r:
+                for _ in range(a.frames):
+                    r.draw_next_frame()
+                    st = r.stats()
+                    ms = st["kernel_ms"]
+                    if best[obj] is None or ms < best[obj]["kernel_ms"]:
+                        best[obj] = {"kernel_ms": ms,
+                                     "msamples_per_s": st["samples"] / (ms * 1e3),
+                                     "segments": st["segments"],
+                                     "group_tests": st["group_tests"],
+                                     "bound_tests": st["bound_tests"]}
+                if rnd == 0:
+                    digest[obj] = hashlib.sha256(r.read_framebuffer().tobytes()).hexdigest()[:16]
+            print(f"round {rnd} {obj}: {best[obj]['msamples_per_s']:.0f} Msamples/s", flush=True)
+    ref = digest[a.objects[0]]
+    out = {o: dict(best[o], sha=digest[o], same_bits=digest[o] == ref) for o in a.objects}
+    print(json.dumps({"config": vars(a), "results": out}, indent=1))
+    if not all(v["same_bits"] for v in out.values()):
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -69,6 +69,7 @@ struct RendererState {
     float cmargin[4] = {0, 0, 0, 0};  // box margin constants (CullTables::margin)
     float4* d_cgroup = nullptr;
     float4* d_cbound = nullptr;
+    float4* d_cbound_nf = nullptr;
     float4* d_cnode = nullptr;
     float4* d_ctop = nullptr;
     // work decomposition
@@ -170,15 +171,40 @@ void free_scene() {
     g.d_material = nullptr;
     if (g.d_cgroup) (void)hipFree(g.d_cgroup);
     if (g.d_cbound) (void)hipFree(g.d_cbound);
+    if (g.d_cbound_nf) (void)hipFree(g.d_cbound_nf);
     if (g.d_cnode) (void)hipFree(g.d_cnode);
     if (g.d_ctop) (void)hipFree(g.d_ctop);
     g.d_cgroup = nullptr;
     g.d_cbound = nullptr;
+    g.d_cbound_nf = nullptr;
     g.d_cnode = nullptr;
     g.d_ctop = nullptr;
     g.ncgroups = 0;
     g.ncbig = 0;
     g.nspheres = 0;
+}
+
+// A pair-SoA box table (cluster.hpp: 16 floats per pair of boxes) in the near/far layout of
+// TraceParams.cbound_nf (20 floats per pair: per axis lo0 lo1 hi0 hi1 lo0 lo1, then K0 K1),
+// uploaded to a new device buffer.
+hipError_t upload_near_far(const std::vector<float>& pairs, float4** out) {
+    const size_t n = pairs.size() / 16;
+    std::vector<float> nf(n * 20);
+    for (size_t i = 0; i < n; i++) {
+        const float* b = &pairs[i * 16];
+        float* o = &nf[i * 20];
+        for (int a = 0; a < 3; a++) {  // lo of axis a at b[2a], hi at b[6 + 2a]
+            o[6 * a + 0] = o[6 * a + 4] = b[2 * a];
+            o[6 * a + 1] = o[6 * a + 5] = b[2 * a + 1];
+            o[6 * a + 2] = b[6 + 2 * a];
+            o[6 * a + 3] = b[6 + 2 * a + 1];
+        }
+        o[18] = b[12];
+        o[19] = b[13];
+    }
+    hipError_t e = hipMalloc(out, sizeof(float) * nf.size());
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*out, nf.data(), sizeof(float) * nf.size(), hipMemcpyHostToDevice);
 }
 
 VkResult bind_kernels() {
@@ -454,6 +480,8 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
                            hipMemcpyHostToDevice));
         VCRT_TRY(hipMemcpy(g.d_cbound, ct.bound.data(), sizeof(float) * ct.bound.size(),
                            hipMemcpyHostToDevice));
+        // near/far layout of the group boxes for the flat scan (vcrt_kernel_abi.h, cbound_nf)
+        VCRT_TRY(upload_near_far(ct.bound, &g.d_cbound_nf));
         VCRT_TRY(hipMemcpy(g.d_cnode, ct.node.data(), sizeof(float) * ct.node.size(),
                            hipMemcpyHostToDevice));
         g.ncgroups = ct.ngroups;
@@ -525,6 +553,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);
         p.cgroup = g.d_cgroup;
         p.cbound = g.d_cbound;
+        p.cbound_nf = g.d_cbound_nf;
         p.cnode = g.d_cnode;
         p.ctop = g.d_ctop;
         p.ncgroups = g.ncgroups;
@@ -556,6 +585,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
         // copy for 16 waves); beyond that from global memory.
         const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
+        const uint32_t tab_lds_flat =
+            static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 5));  // cbound_nf
         const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
         const bool lane_wide = lane_lds && tab_lds > 32768u;
         int variant = g.desc.kernel_variant;
@@ -576,7 +607,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         // the flat scan keeps 4 KB of stacks per wave in LDS (4 waves per block), beside its
         // tables when they fit in 32 KB (16-bit entries); otherwise the tables stay in global
         // memory and the stacks take 32-bit entries (6.25 KB per wave)
-        const bool flat_lds = lane_lds && !lane_wide && g.ncgroups <= vcrt::kFlatMaxGroups;
+        const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
+                              g.ncgroups <= vcrt::kFlatMaxGroups;
         hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
         uint32_t lds = 0;
         if (variant == VCRT_KERNEL_LDS) {
@@ -589,7 +621,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_lds) {
             f = g.k_trace_cull_flat;
             fs = g.k_trace_cull_flat_stats;
-            lds = tab_lds + 4 * vcrt::kWaveScratchBytes;
+            lds = tab_lds_flat + 4 * vcrt::kWaveScratchBytes;
         } else if (variant == VCRT_KERNEL_CULL_FLAT) {
             f = g.k_trace_cull_flat_global;
             fs = g.k_trace_cull_flat_global_stats;

@@ -472,6 +472,51 @@ __device__ __forceinline__ uint32_t push_bound_pair(uint32_t acc, const BoxRay& 
     return push_sign(push_sign(acc, D.y), D.x);
 }
 
+// Box test of a group pair in the near/far layout (TraceParams.cbound_nf). For inv = 1/d' > 0
+// the exact products order lo*inv <= hi*inv and rounding is monotone, so fma(lo, inv, c) <=
+// fma(hi, inv, c): box_gap's per-axis min / max are the lo / hi plane when inv > 0 and the hi / lo
+// plane when inv < 0 (d' is never 0). Each axis stores (lo, hi, lo), so the near plane sits at
+// byte 8 * sign(inv) of the axis and the far plane 8 bytes after it: one per-lane address per
+// axis, one ds_read2_b64 per axis and pair. The gap is box_gap's value (at most the sign of a
+// zero tf - tn differs, and adding the slack c1 >= +0 gives the same sum for either zero), for
+// one v_max3 + one v_min3 per box instead of 3 min + 3 max + max3 + min3.
+struct NearFarAddr {
+    const char* x;  // near plane of axis x of pair 0 (far: + 8 bytes)
+    const char* y;
+    const char* z;
+    const char* k;  // (K0, K1) of pair 0
+};
+
+__device__ __forceinline__ NearFarAddr near_far_addr(const float4* pairs, float ix, float iy,
+                                                     float iz) {
+    const char* b = reinterpret_cast<const char*>(pairs);
+    NearFarAddr a;
+    a.x = b + ((__float_as_uint(ix) >> 31) << 3);
+    a.y = b + 24 + ((__float_as_uint(iy) >> 31) << 3);
+    a.z = b + 48 + ((__float_as_uint(iz) >> 31) << 3);
+    a.k = b + 72;
+    return a;
+}
+
+__device__ __forceinline__ v2f ld2(const char* p) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    return (v2f){v.x, v.y};
+}
+
+__device__ __forceinline__ uint32_t push_bound_pair_nf(uint32_t acc, const BoxRay& r,
+                                                       const NearFarAddr& a, int off) {
+    const v2f tnx = vfma(ld2(a.x + off), r.ix, r.cx), tfx = vfma(ld2(a.x + off + 8), r.ix, r.cx);
+    const v2f tny = vfma(ld2(a.y + off), r.iy, r.cy), tfy = vfma(ld2(a.y + off + 8), r.iy, r.cy);
+    const v2f tnz = vfma(ld2(a.z + off), r.iz, r.cz), tfz = vfma(ld2(a.z + off + 8), r.iz, r.cz);
+    v2f tn, tf;
+    tn.x = fmaxf(fmaxf(tnx.x, tny.x), tnz.x);
+    tn.y = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
+    tf.x = fminf(fminf(tfx.x, tfy.x), tfz.x);
+    tf.y = fminf(fminf(tfx.y, tfy.y), tfz.y);
+    const v2f D = vfma(ld2(a.k + off), r.c2, (tf - tn) + r.c1);
+    return push_sign(push_sign(acc, D.y), D.x);
+}
+
 // Sign bit set when a member may be accepted: disc >= 0 and (hb < 0 or cc < 0), by sign bits
 // (a -0 hb only adds a candidate that the exact test then rejects; disc is never -0).
 __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
@@ -579,11 +624,11 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         r.cz = (v2f){cz, cz};
         r.c1 = (v2f){c1, c1};
         r.c2 = (v2f){c2, c2};
-        const float4* gb = tbound + 16u * (e & F::kMask);
+        const float4* gb = tbound + 20u * (e & F::kMask);  // 4 pairs x 80 B
+        const NearFarAddr na = near_far_addr(gb, ix, iy, iz);
         uint32_t gout = 0;
 #pragma unroll
-        for (int k = 3; k >= 0; k--)
-            gout = push_bound_pair(gout, r, gb[4 * k], gb[4 * k + 1], gb[4 * k + 2], gb[4 * k + 3]);
+        for (int k = 3; k >= 0; k--) gout = push_bound_pair_nf(gout, r, na, 80 * k);
         uint32_t need = act ? (~gout & 0xffu) : 0u;
         uint32_t tot;
         uint32_t pos = pushed + wave_prefix<4>((uint32_t)__popc(need), tot);
@@ -751,8 +796,8 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             if (__ballot(in_chunk) == 0) continue;
             // level 1, wave-uniform: nodes of this chunk, per-lane bits -> node entries
             const int nn = min(8, (ncg - base) >> 3);
-            cfloat4* nb = node + 4 * (base >> 4);
             uint32_t out = 0;
+            cfloat4* nb = node + 4 * (base >> 4);
             BoundPair cur = load_bound_pair(nb + 4 * ((nn - 2) >> 1));
             for (int j = nn - 2; j >= 0; j -= 2) {
                 const BoundPair nxt = load_bound_pair(nb + 4 * ((j >= 2 ? j - 2 : j) >> 1));
@@ -923,15 +968,18 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = p.geom[i];
         __syncthreads();
     }
-    const float4* tbound = p.cbound;
+    // group-pair boxes: the flat scan reads the near/far layout (80 B per pair), the others
+    // the pair-SoA one (64 B)
+    constexpr bool kNearFar = kCull == 4 || kCull == 5;
+    const float4* tbound = kNearFar ? p.cbound_nf : p.cbound;
     const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
     // the flat scan's stacks: after the LDS tables (kCull 4), or alone with the tables in
     // global memory and 32-bit entries (kCull 5)
     constexpr bool kWide = kCull == 5;
     WaveScratch<kWide>* ws = nullptr;
     if constexpr (kCull == 2 || kCull == 4) {
-        const int nb = (p.ncgroups >> 1) * 4, ng = p.ncgroups * 5;
-        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = p.cbound[i];
+        const int nb = (p.ncgroups >> 1) * (kNearFar ? 5 : 4), ng = p.ncgroups * 5;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = tgroup[i];
         __syncthreads();
         tbound = lds_geom;

@@ -39,6 +39,9 @@ struct TraceParams {
     const float4* cbound;   // [ncgroups / 2 * 4] boxes of group pairs, pair-SoA:
                             //   (lox0,lox1,loy0,loy1) (loz0,loz1,hix0,hix1) (hiy0,hiy1,hiz0,hiz1)
                             //   (K0,K1,0,0), K = 8.1u / r_min of the box's members
+    const float4* cbound_nf;  // [ncgroups / 2 * 5] the same group-pair boxes for the flat
+                              //   scan's near/far reads: per axis (lo0,lo1,hi0,hi1,lo0,lo1),
+                              //   x then y then z, then (K0,K1) -- 80 B per pair
     const float4* cnode;    // [ncgroups / 16 * 4] boxes of node pairs (8 groups per node)
     const float4* ctop;     // boxes of pairs of 64-group chunks, same form
     float box_margin[4];    // max |centre|, r_max^2, max |box coordinate|, 0 (rounded up)
