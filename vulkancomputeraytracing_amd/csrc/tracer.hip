@@ -568,10 +568,23 @@ __device__ __forceinline__ unsigned long long pack_hit(float t, int idx) {
     return ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)idx;
 }
 
-// Exclusive prefix over the active lanes of a per-lane count c < 2^kBits, and the wave total
-// (bit-sliced ballots: 4 VALU per bit).
+// Exclusive prefix over the active lanes of a per-lane count c < 2^kBits, and the wave total.
+// With every lane active: an inclusive DPP scan (row_shr 1/2/4/8, row_bcast 15/31; 8 VALU).
+// Otherwise (the drain at the end of the grid, where finished lanes are masked off and DPP
+// would read their stale registers): bit-sliced ballots, ~5 VALU per bit.
 template <int kBits>
 __device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
+    if (__builtin_amdgcn_read_exec() == ~0ull) {
+        int x = (int)c;
+        x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+        x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+        x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+        x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+        x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+        x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+        total = (uint32_t)__builtin_amdgcn_readlane(x, 63);
+        return (uint32_t)x - c;
+    }
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int b = 0; b < kBits; ++b) {
