@@ -50,6 +50,21 @@ traffic[key] = {"hbm_bytes_per_launch": per_launch, "kernel": kernel, "fetch_kb"
                 "write_kb": write["sum"] / write["dispatches"], "round": tag,
                 "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/render_once.py "
                         "at the bench config; FETCH_SIZE doubled (gfx950 correction)"}
+# VALUBusy / VALUUtilization (rocprofiler-sdk counter_defs.yaml, gfx950 rows):
+#   100 * SQ_ACTIVE_INST_VALU / CU_NUM / max(GRBM_GUI_ACTIVE), max over the 8 XCDs = sum / 8
+#   100 * SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64)
+sq1, sq2 = summary.get("pmc_sq1", {}), summary.get("pmc_sq2", {})
+try:
+    valu = sq2[f"{kernel}|SQ_ACTIVE_INST_VALU"]["sum"]
+    thread = sq2[f"{kernel}|SQ_THREAD_CYCLES_VALU"]["sum"]
+    gui = sq1[f"{kernel}|GRBM_GUI_ACTIVE"]["sum"] / 8
+    traffic[key]["valu_busy_pct"] = round(100 * valu / 256 / gui, 1)
+    traffic[key]["valu_utilization_pct"] = round(100 * thread / (valu * 64), 1)
+    traffic[key]["valu_note"] = ("VALUBusy = 100 SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8 "
+                                 "XCDs); VALUUtilization = 100 SQ_THREAD_CYCLES_VALU / "
+                                 "(SQ_ACTIVE_INST_VALU x 64): active lanes per VALU instruction")
+except KeyError:
+    pass
 with open(traffic_path, "w") as f:
     json.dump(traffic, f, indent=1)
 print(json.dumps(traffic[key]))
