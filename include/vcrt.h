@@ -198,6 +198,14 @@ int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom,
                          float* node, float* top, int32_t* index, int32_t* big_groups,
                          float* margin4, int32_t cap_groups);
 
+/* Device self-test of the kernel's fast sin path (tracer.hip vcrt_check_sin): for the fp32
+ * inputs whose bit patterns are first .. first + count - 1, counts those where the device's
+ * sin_fast differs from the canonical sin (must be 0) and those where it fell back to the
+ * canonical evaluation, and returns the smallest differing pattern (0xFFFFFFFF if none).
+ * Diagnostic addition (the reference has no such call). Requires vcrt_begin. */
+vcrt_result vcrt_selftest_sin(uint32_t first, uint32_t count, uint64_t* mismatches,
+                              uint64_t* fallbacks, uint32_t* first_mismatch);
+
 /* Canonical math as used by the kernel (host evaluation), for tests and tools. */
 float vcrt_canonical_sin(float x);
 float vcrt_canonical_rand(float x, float y);

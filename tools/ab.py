@@ -9,14 +9,17 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# VCRT_PKG_ROOT: import the package (and its libvcrt.so) from another tree, e.g. a build of an
+# earlier commit, to compare across ABI changes (one tree per process)
+sys.path.insert(0, os.environ.get("VCRT_PKG_ROOT",
+                                  os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import vulkancomputeraytracing_amd as vc  # noqa: E402
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("objects", nargs="+")
+    p.add_argument("objects", nargs="+", help="code objects, or 'default' for the package's own")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spp", type=int, default=256)
@@ -32,7 +35,7 @@ def main():
         for obj in a.objects:
             desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
                                  max_depth=a.depth, kernel_variant=a.variant, device=0,
-                                 code_object_path=obj)
+                                 code_object_path=None if obj == "default" else obj)
             with vc.Renderer(desc, a.scene) as r:
                 for _ in range(a.frames):
                     r.draw_next_frame()

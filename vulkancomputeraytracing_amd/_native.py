@@ -121,6 +121,10 @@ SIGNATURES = {
     "vcrt_get_stats": (ctypes.c_int32, [ctypes.POINTER(vcrt_stats)]),
     "vcrt_reset_accumulation": (ctypes.c_int32, []),
     "vcrt_read_framebuffer_srgb8": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_size_t]),
+    "vcrt_selftest_sin": (ctypes.c_int32, [ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_uint32)]),
     "vcrt_srgb8_thresholds": (None, [ctypes.c_void_p]),
     "vcrt_shader_load": (ctypes.c_int32, [ctypes.c_char_p]),
     "vcrt_scene_builtin": (ctypes.c_int32,

@@ -795,6 +795,33 @@ vcrt_result vcrt_reset_accumulation(void) {
     return VCRT_SUCCESS;
 }
 
+vcrt_result vcrt_selftest_sin(uint32_t first, uint32_t count, uint64_t* mismatches,
+                              uint64_t* fallbacks, uint32_t* first_mismatch) {
+    if (!g.begun || !mismatches || !fallbacks || !first_mismatch)
+        return VCRT_ERROR_INITIALIZATION_FAILED;
+    hipFunction_t f = nullptr;
+    VCRT_TRY(hipModuleGetFunction(&f, static_cast<hipModule_t>(g.stage.module), "vcrt_check_sin"));
+    void* buf = nullptr;  // [2] counters + first mismatch
+    VCRT_TRY(hipMalloc(&buf, 24));
+    uint32_t init[6] = {0, 0, 0, 0, 0xFFFFFFFFu, 0};
+    hipError_t e = hipMemcpy(buf, init, sizeof(init), hipMemcpyHostToDevice);
+    vcrt::SinCheckParams sp{static_cast<unsigned long long*>(buf),
+                            reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + 16), first, count};
+    VkResult r = e == hipSuccess ? launch(f, 8 * 256 * 8, 256, 0, sp) : to_vk(e);
+    uint32_t out[6] = {0, 0, 0, 0, 0, 0};
+    if (r == VK_SUCCESS) {
+        e = hipMemcpyAsync(out, buf, sizeof(out), hipMemcpyDeviceToHost, g.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(g.stream);
+        r = to_vk(e);
+    }
+    (void)hipFree(buf);
+    if (r != VK_SUCCESS) return r;
+    std::memcpy(mismatches, &out[0], 8);
+    std::memcpy(fallbacks, &out[2], 8);
+    *first_mismatch = out[4];
+    return VCRT_SUCCESS;
+}
+
 vcrt_result vcrt_read_framebuffer_srgb8(uint8_t* rgba8, size_t bytes) {
     if (!g.begun || (!rgba8 && g.local_elems)) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (bytes < static_cast<size_t>(g.local_elems) * 4) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;

@@ -1138,11 +1138,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             const int type = (int)mat;
             const f3 albedo = mk(sh.x, sh.y, sh.z);
             const float param = sh.w;
-            // first rand: rand(dir.xy) for lambertian/metal, rand(point.xy) for glass
-            const float r1 = (type == 3) ? rand2(point.x, point.y) : rand2(d.x, d.y);
+            // rand(dir.xy), rand(dir.xz), rand(dir.yz) for lambertian/metal (functions.glsl:43),
+            // rand(point.xy) for glass (textures.glsl:51): three sines for every hit lane
+            float s1, s2, s3;
+            sin3((type == 3) ? rand_arg(point.x, point.y) : rand_arg(d.x, d.y),
+                 rand_arg(d.x, d.z), rand_arg(d.y, d.z), s1, s2, s3);
+            const float r1 = rand_of_sin(s1);
             if (type == 1 || type == 2) {
-                const float r2 = rand2(d.x, d.z);
-                const float r3 = rand2(d.y, d.z);
+                const float r2 = rand_of_sin(s2);
+                const float r3 = rand_of_sin(s3);
                 const f3 u = normalize(mk(r1, r2, r3));  // random_in_unit_sphere(dir)
                 if (type == 1) {
                     d = add(normal, u);
@@ -1395,6 +1399,38 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_encode_srgb8(EncodeParams
         }
         const float a = v.w != v.w ? 0.0f : fminf(fmaxf(v.w, 0.0f), 1.0f);
         p.out[i] = make_uchar4(b[0], b[1], b[2], (unsigned char)(a * 255.0f + 0.5f));
+    }
+}
+
+// Self-test of sin_fast (vcrt_math.h) against sin_canonical on the fp32 inputs with bit
+// patterns first .. first + count - 1 (wrapping): counts the inputs where they differ and where
+// the fast value was not accepted (the fallback ran), and keeps the smallest differing pattern.
+extern "C" __global__ __launch_bounds__(256) void vcrt_check_sin(SinCheckParams p) {
+    uint64_t bad = 0, fallback = 0;
+    uint32_t first_bad = 0xFFFFFFFFu;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.count; i += stride) {
+        const uint32_t bits = p.first + i;
+        const float x = __uint_as_float(bits);
+        float f;
+        const bool ok = sin_fast_try(x, f);
+        if (!ok) f = sin_canonical(x);
+        fallback += ok ? 0u : 1u;
+        const float want = sin_canonical(x);
+        if (__float_as_uint(f) != __float_as_uint(want)) {
+            ++bad;
+            first_bad = min(first_bad, bits);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        bad += __shfl_xor(bad, off);
+        fallback += __shfl_xor(fallback, off);
+        first_bad = min(first_bad, (uint32_t)__shfl_xor((int)first_bad, off));
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        if (bad) atomicAdd(p.result + 0, (unsigned long long)bad);
+        if (fallback) atomicAdd(p.result + 1, (unsigned long long)fallback);
+        if (first_bad != 0xFFFFFFFFu) atomicMin(p.first_bad, first_bad);
     }
 }
 

@@ -91,6 +91,12 @@ struct EncodeParams {
     uint32_t count;
 };
 
+struct SinCheckParams {
+    unsigned long long* result;  // [2]: inputs where sin_fast != sin_canonical, fallbacks
+    uint32_t* first_bad;         // smallest differing bit pattern (init 0xFFFFFFFF)
+    uint32_t first, count;       // input bit patterns first .. first + count - 1
+};
+
 struct FillParams {
     float4* out;
     uint32_t count;

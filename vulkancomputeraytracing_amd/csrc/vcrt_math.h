@@ -182,11 +182,101 @@ VCRT_HD float sin_canonical(float xf) {
     return (float)s;
 }
 
-// functions.glsl:10-12  rand(co) = fract(sin(dot(co, vec2(12.9898,78.233))) * 43758.5453)
+#if defined(__HIP_DEVICE_COMPILE__)
+// The canonical sin on the device, by Ziv's method: one branch-free evaluation for every lane
+// (sin_canonical evaluates both fdlibm kernels under divergence, since the quadrant varies per
+// lane), accepted when it provably rounds to the same fp32 as sin_canonical, else
+// sin_canonical itself. Fast value s: x reduced modulo pi (k = rint(x / pi); r = x - k pi with
+// pi split as pi_hi (33 bits: k pi_hi exact for |k| < 2^20) + pi_mid, FMAs), then Taylor to r^21
+// on |r| <= pi/2 (truncation < 2^-59.4), sign (-1)^k. For |x| < 2^19 and |r| >= 2^-12 the error
+// of s and that of sin_canonical's double result (2-term Cody-Waite reduction, fdlibm kernels)
+// are each below 2^-48 |sin x|; if s lies farther than 2^-44 |s| from every fp32 rounding
+// boundary, both round to the same float f. Otherwise (|r| < 2^-12, |x| >= 2^19, f a power of
+// two, or s near a boundary: ~2e-4 of the calls) the lane takes sin_canonical.
+// tests/test_gpu_parity.py::test_sin_fast_exhaustive compares the two on all 2^32 inputs.
+// A double constant materialised in an SGPR pair where it is used: plain literals get hoisted
+// out of the tracer's loops into VGPR pairs, which then spill (v_fma_f64 takes no 64-bit
+// literal on gfx950).
+template <uint64_t kBits>
+__device__ __forceinline__ double sconst() {
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)kBits));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(kBits >> 32)));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+#define VCRT_DC(x) sconst<__builtin_bit_cast(uint64_t, (double)(x))>()
+
+__device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
+    const double x = (double)xf;
+    const double k = __builtin_rint(x * VCRT_DC(0.31830988618379067154));
+    double r = __builtin_fma(-k, VCRT_DC(0x1.921fb544p+1), x);
+    r = __builtin_fma(-k, VCRT_DC(0x1.0b4611a626331p-33), r);
+    const double r2 = r * r;
+    double p = VCRT_DC(0x1.71b8ef6dcf572p-66);  // (-1)^j / (2j+1)!, j = 10 .. 1
+    p = __builtin_fma(p, r2, VCRT_DC(-0x1.2f49b46814157p-57));
+    p = __builtin_fma(p, r2, VCRT_DC(0x1.952c77030ad4ap-49));
+    p = __builtin_fma(p, r2, VCRT_DC(-0x1.ae7f3e733b81fp-41));
+    p = __builtin_fma(p, r2, VCRT_DC(0x1.6124613a86d09p-33));
+    p = __builtin_fma(p, r2, VCRT_DC(-0x1.ae64567f544e4p-26));
+    p = __builtin_fma(p, r2, VCRT_DC(0x1.71de3a556c734p-19));
+    p = __builtin_fma(p, r2, VCRT_DC(-0x1.a01a01a01a01ap-13));
+    p = __builtin_fma(p, r2, VCRT_DC(0x1.1111111111111p-7));
+    p = __builtin_fma(p, r2, VCRT_DC(-0x1.5555555555555p-3));
+    double s = __builtin_fma(r * r2, p, r);
+    if ((int)k & 1) s = -s;
+    const float f = (float)s;
+    const uint32_t fb = __builtin_bit_cast(uint32_t, f);
+    // distance from s to the nearest rounding boundary of f (f normal: |f| > 2^-13)
+    const double half_ulp = __builtin_ldexp(1.0, __builtin_amdgcn_frexp_expf(f) - 25);
+    const double margin = half_ulp - __builtin_fabs(s - (double)f);
+    out = f;
+    const bool ok = __builtin_fabsf(xf) < 0x1p19f && __builtin_fabs(r) >= 0x1p-12 &&
+                    (fb & 0x7FFFFFu) != 0u && margin > 0x1p-44 * __builtin_fabs(s);
+#if VCRT_SINSB
+    __builtin_amdgcn_sched_barrier(0);  // one evaluation at a time: the three rand() calls of a
+                                        // diffuse hit interleaved would spill VGPRs
+#endif
+    return ok;
+}
+
+// The three rand() values of a scatter (textures.glsl:21, :51, functions.glsl:43): sines of
+// a1..a3 by sin_fast_try; a lane whose fast value was not accepted recomputes all three
+// canonically in one loop (one inlined copy of the fdlibm path instead of three).
+__device__ __forceinline__ void sin3(float a1, float a2, float a3, float& s1, float& s2,
+                                     float& s3) {
+    const bool ok1 = sin_fast_try(a1, s1), ok2 = sin_fast_try(a2, s2), ok3 = sin_fast_try(a3, s3);
+    if (!(ok1 && ok2 && ok3)) {
+#pragma nounroll
+        for (int j = 0; j < 3; ++j) {
+            const float c = sin_canonical(j == 0 ? a1 : j == 1 ? a2 : a3);
+            s1 = j == 0 ? c : s1;
+            s2 = j == 1 ? c : s2;
+            s3 = j == 2 ? c : s3;
+        }
+    }
+}
+
+__device__ __forceinline__ float sin_fast(float xf) {
+    float f;
+    if (!sin_fast_try(xf, f)) f = sin_canonical(xf);
+    return f;
+}
+#endif
+
+// functions.glsl:10-12  rand(co) = fract(sin(dot(co, vec2(12.9898,78.233))) * 43758.5453),
+// split as the sine's argument and the fract of the scaled sine
+VCRT_HD float rand_arg(float x, float y) { return x * 12.9898f + y * 78.233f; }
+VCRT_HD float rand_of_sin(float s) {
+    const float p = s * 43758.5453f;
+    return p - __builtin_floorf(p);
+}
+
 VCRT_HD float rand2(float x, float y) {
-    float arg = x * 12.9898f + y * 78.233f;
+    float arg = rand_arg(x, y);
 #ifdef VCRT_EXPERIMENT_FAST_SIN  // timing experiments only: not the canonical value
     float p = __builtin_sinf(arg) * 43758.5453f;
+#elif defined(__HIP_DEVICE_COMPILE__)
+    float p = sin_fast(arg) * 43758.5453f;
 #else
     float p = sin_canonical(arg) * 43758.5453f;
 #endif
