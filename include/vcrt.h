@@ -127,7 +127,8 @@ typedef struct vcrt_stats {
                            end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,
                            its uniform levels, node / group / candidate passes (CULL_FLAT),
                            candidate passes run, the whole wave, the big list, node pushes,
-                           [17..18] shading and sky, block fetch */
+                           [17..18] shading and sky, block fetch; [19..22] flat passes:
+                           entries dealt, live lanes offered, partial passes, passes */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

@@ -18,4 +18,7 @@ for name, k in (("scan", 8), ("big list", 15), ("levels", 9), ("node pushes", 16
 print("cand passes per wave-iter %.2f; node %.2f group %.2f (from counters)" % (
     d[13] / wi, (st["bound_tests"] / wi), st["group_tests"] / wi))
 print("total ticks per wave-iter %.1f" % (tot / wi))
+if len(d) > 22 and d[22]:
+    print("flat passes per wave-iter %.2f, partial %.2f; entries per live lane %.3f" % (
+        d[22] / wi, d[21] / wi, d[19] / d[20]))
 PY

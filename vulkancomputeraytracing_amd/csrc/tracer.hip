@@ -537,8 +537,9 @@ __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
 // one address: 9x the LDS bank conflicts of the per-lane scan, 9% slower overall.) Every owner's
 // (t, sphere index) minimum is an LDS 64-bit word updated with ds_min_u64: the lexicographic
 // minimum of (t, index) is what `consider` computes, since t > 0 orders like its bit pattern.
-// Passes drain candidates first, then groups, then nodes, which bounds every stack:
-// < 64 left over + at most 8 x 64 (node, group) or 4 x 64 (cand) pushed by one pass.
+// A pass pushes onto the next stack only while that stack holds < nact <= 64 entries (full
+// passes run deepest stack first; the final drain's partial passes run top-down), which bounds
+// every stack: < 64 left over + at most 8 x 64 (node, group) or 4 x 64 (cand) pushed by one pass.
 constexpr int kNodeCap = 576;
 constexpr int kGroupCap = 576;
 constexpr int kCandCap = 320;
@@ -711,6 +712,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
 struct PhaseTicks {
     uint64_t scan = 0, levels = 0, node = 0, group = 0, cand = 0, cand_passes = 0, big = 0,
              push = 0, shade = 0, fetch = 0;
+    uint64_t pass_entries = 0, pass_lanes = 0, partial_passes = 0, passes = 0;
 };
 
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
@@ -730,18 +732,38 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
     for (;;) {
         __builtin_amdgcn_wave_barrier();  // the entries were written by other lanes
         uint64_t t0 = 0;
-        if constexpr (kStats) t0 = ticks();
-        if (nc >= th) {
+        if constexpr (kStats) {
+            t0 = ticks();
+            const uint32_t n = nc >= nact ? nc : ng >= nact ? ng : nn >= nact ? nn
+                             : th == 1u ? (nn ? nn : ng ? ng : nc) : 0u;
+            if (n) {
+                pt.pass_entries += min(n, nact);
+                pt.pass_lanes += nact;
+                pt.partial_passes += n < nact;
+                ++pt.passes;
+            }
+        }
+        // full passes first, deepest stack first; then (final drain only) the partial passes
+        // top-down, nodes before groups before candidates, so that each level's remainder
+        // joins the next level's before that one runs: ~3 partial passes per segment instead
+        // of a cascade. A pass onto a stack runs only while that stack holds < nact <= 64
+        // entries, which keeps the caps (see kNodeCap).
+        int kind = -1;
+        if (nc >= nact) kind = 0;
+        else if (ng >= nact) kind = 1;
+        else if (nn >= nact) kind = 2;
+        else if (th == 1u) kind = nn ? 2 : ng ? 1 : nc ? 0 : -1;
+        if (kind == 0) {
             flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tgroup, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
-        } else if (ng >= th) {
+        } else if (kind == 1) {
             ++n_groups;
             flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tgroup, my);
             if constexpr (kStats) pt.group += ticks() - t0;
-        } else if (nn >= th) {
+        } else if (kind == 2) {
             n_bounds += 8;
             flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tgroup, my);
             if constexpr (kStats) pt.node += ticks() - t0;
@@ -1246,6 +1268,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             atomicAdd(p.debug + 16, (unsigned long long)pt.push);
             atomicAdd(p.debug + 17, (unsigned long long)pt.shade);
             atomicAdd(p.debug + 18, (unsigned long long)pt.fetch);
+            atomicAdd(p.debug + 19, (unsigned long long)pt.pass_entries);
+            atomicAdd(p.debug + 20, (unsigned long long)pt.pass_lanes);
+            atomicAdd(p.debug + 21, (unsigned long long)pt.partial_passes);
+            atomicAdd(p.debug + 22, (unsigned long long)pt.passes);
         }
     }
 }
