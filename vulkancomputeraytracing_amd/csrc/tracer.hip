@@ -1051,6 +1051,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
         uint64_t t_fetch = 0;
         if constexpr (kStats) t_fetch = ticks();
+        // The loop only hands out slots; the lane state is set up once after it (setting it up
+        // inside made the compiler copy ~20 live registers around the loop on every pass).
+        bool got = false;
+        uint32_t g_lt = 0u, g_chunk = 0u, g_slot = 0u, g_px = 0u, g_py = 0u;
         uint64_t need_mask = __ballot(need && !done);
         while (need_mask) {
             if (blk_next >= 64u) {
@@ -1076,26 +1080,34 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                 const uint32_t slot = blk_next + mine;
                 const uint32_t px = 8u * blk_tx + (slot & 7u), py = 8u * blk_ty + (slot >> 3);
                 if (px < (uint32_t)p.width && py < (uint32_t)p.height) {  // edge tiles: skip
-                    chunk = blk_chunk;
-                    q = blk_lt * 64u + slot;
-                    out_index = p.world == 1 ? py * (uint32_t)p.width + px : q;
-                    // shader.comp:43  pixel00 + x*delta_u + y*delta_v
-                    pc = add(add(p00, scale((float)px, du)), scale((float)py, dv));
-                    acc = mk(0.f, 0.f, 0.f);
-                    sample = (int)(chunk * (uint32_t)p.chunk);
-                    sample_end = min(sample + p.chunk, p.spp);
-                    // first camera ray of the chunk, shader.comp:48-52
-                    const float2 jt = p.jitter[sample];
-                    const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
-                    o = cam;
-                    d = sub(ps, cam);
-                    atten = mk(1.f, 1.f, 1.f);
-                    pass = 0;
+                    got = true;
+                    g_lt = blk_lt;
+                    g_chunk = blk_chunk;
+                    g_slot = slot;
+                    g_px = px;
+                    g_py = py;
                     need = false;
                 }
             }
             blk_next += min((uint32_t)__popcll(need_mask), avail);
             need_mask = __ballot(need && !done);
+        }
+        if (got) {
+            chunk = g_chunk;
+            q = g_lt * 64u + g_slot;
+            out_index = p.world == 1 ? g_py * (uint32_t)p.width + g_px : q;
+            // shader.comp:43  pixel00 + x*delta_u + y*delta_v
+            pc = add(add(p00, scale((float)g_px, du)), scale((float)g_py, dv));
+            acc = mk(0.f, 0.f, 0.f);
+            sample = (int)(chunk * (uint32_t)p.chunk);
+            sample_end = min(sample + p.chunk, p.spp);
+            // first camera ray of the chunk, shader.comp:48-52
+            const float2 jt = p.jitter[sample];
+            const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
+            o = cam;
+            d = sub(ps, cam);
+            atten = mk(1.f, 1.f, 1.f);
+            pass = 0;
         }
         if constexpr (kStats) pt.fetch += ticks() - t_fetch;
         const uint64_t live = __ballot(!done);

@@ -206,6 +206,15 @@ __device__ __forceinline__ double sconst() {
 }
 #define VCRT_DC(x) sconst<__builtin_bit_cast(uint64_t, (double)(x))>()
 
+// fma(a, b, c) with c an SGPR pair, as one VOP3 v_fma_f64. The compiler otherwise picks the
+// two-address v_fmac_f64, which needs the addend in the destination: two v_mov_b32 per
+// Horner step of sin_fast_try (20 of its ~45 VALU instructions).
+__device__ __forceinline__ double fma_vvs(double a, double b, double c) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+}
+
 __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
     const double x = (double)xf;
     const double k = __builtin_rint(x * VCRT_DC(0.31830988618379067154));
@@ -213,15 +222,15 @@ __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
     r = __builtin_fma(-k, VCRT_DC(0x1.0b4611a626331p-33), r);
     const double r2 = r * r;
     double p = VCRT_DC(0x1.71b8ef6dcf572p-66);  // (-1)^j / (2j+1)!, j = 10 .. 1
-    p = __builtin_fma(p, r2, VCRT_DC(-0x1.2f49b46814157p-57));
-    p = __builtin_fma(p, r2, VCRT_DC(0x1.952c77030ad4ap-49));
-    p = __builtin_fma(p, r2, VCRT_DC(-0x1.ae7f3e733b81fp-41));
-    p = __builtin_fma(p, r2, VCRT_DC(0x1.6124613a86d09p-33));
-    p = __builtin_fma(p, r2, VCRT_DC(-0x1.ae64567f544e4p-26));
-    p = __builtin_fma(p, r2, VCRT_DC(0x1.71de3a556c734p-19));
-    p = __builtin_fma(p, r2, VCRT_DC(-0x1.a01a01a01a01ap-13));
-    p = __builtin_fma(p, r2, VCRT_DC(0x1.1111111111111p-7));
-    p = __builtin_fma(p, r2, VCRT_DC(-0x1.5555555555555p-3));
+    p = fma_vvs(p, r2, VCRT_DC(-0x1.2f49b46814157p-57));
+    p = fma_vvs(p, r2, VCRT_DC(0x1.952c77030ad4ap-49));
+    p = fma_vvs(p, r2, VCRT_DC(-0x1.ae7f3e733b81fp-41));
+    p = fma_vvs(p, r2, VCRT_DC(0x1.6124613a86d09p-33));
+    p = fma_vvs(p, r2, VCRT_DC(-0x1.ae64567f544e4p-26));
+    p = fma_vvs(p, r2, VCRT_DC(0x1.71de3a556c734p-19));
+    p = fma_vvs(p, r2, VCRT_DC(-0x1.a01a01a01a01ap-13));
+    p = fma_vvs(p, r2, VCRT_DC(0x1.1111111111111p-7));
+    p = fma_vvs(p, r2, VCRT_DC(-0x1.5555555555555p-3));
     double s = __builtin_fma(r * r2, p, r);
     if ((int)k & 1) s = -s;
     const float f = (float)s;
