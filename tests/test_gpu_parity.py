@@ -423,3 +423,28 @@ def test_sin_fast_exhaustive():
     # the fallback is rare for the arguments rand() sees, but counts every input >= 2^19, NaN
     # and inf (about 3/4 of all bit patterns)
     assert total_fallback < (1 << 32)
+
+
+def test_bench_multirank_gather_bitwise():
+    """bench.py's N-rank path end to end on one GPU (3 ranks rendering their tile shares in
+    turn, gloo standing in for RCCL, which refuses two ranks on one device): the frame gathered
+    to rank 0 and re-interleaved by vcrt_assemble is bit-identical to a 1-GPU render."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, VCRT_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"),
+           "--gpus", "3", "--steps", "1", "--warmup", "0", "--width", "200", "--height", "120",
+           "--spp", "8", "--depth", "10", "--scene", "final", "--no-cpu-baseline", "--validate"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 3
+    assert res["validated_bitwise_vs_1gpu"] is True

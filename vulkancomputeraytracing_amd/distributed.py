@@ -4,7 +4,7 @@ One process per GPU. The frame is cut into 8x8 tiles (tx, ty); rank r renders th
 (tx + ty) % world == r, so every work item stays a coherent 8x8 tile and every rank gets the
 same number of tiles (to one per row) spread over every row and column of the frame (sky and
 ground, left and right alike: SURVEY.md 8(e)).
-The packed rank framebuffers [tiles_per_rank][64] are all-gathered over RCCL
+The packed rank framebuffers [tiles_per_rank][64] are gathered to rank 0 over RCCL
 (``torch.distributed`` backend "nccl") and rank 0 re-interleaves them with the vcrt_assemble
 HIP kernel. The reference is single-GPU (Environment.cpp:157-165; "TODO: Cross-GPU sharing",
 Frontend.cpp:107); the gather is the one exchange step of the path.
@@ -19,20 +19,31 @@ def tiles_per_rank(width: int, height: int, world: int) -> int:
     return max(len(tiles_for_rank(width, height, world, r)) for r in range(world))
 
 
-def gather_tiles(local, tiles_pad: int, group=None):
-    """All-gather the ranks' packed tile framebuffers. `local` is [tiles_pad * 64, 4] float
-    (tiles past the rank's own count are padding). Returns [world * tiles_pad * 64, 4],
-    rank-major."""
+def gather_tiles(local, tiles_pad: int, group=None, dst: int = 0):
+    """Gather the ranks' packed tile framebuffers to rank `dst`. `local` is
+    [tiles_pad * 64, 4] float (tiles past the rank's own count are padding). Returns
+    [world * tiles_pad * 64, 4], rank-major, on `dst` and None elsewhere.
+
+    A gather, not an all-gather: only `dst` assembles the frame. Over RCCL it is one grouped
+    send/recv per peer, so `dst` receives from all peers at once over their own xGMI links
+    (1/world of the frame each) instead of a world-1 step ring that moves the whole frame
+    through every rank."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     assert local.shape[0] == tiles_pad * 64 and local.is_contiguous()
     if local.is_cuda and dist.get_backend(group) == "gloo":
         # rehearsal path (several ranks on one GPU): gloo gathers host copies
-        return gather_tiles(local.cpu(), tiles_pad, group).to(local.device)
-    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                      device=local.device)
-    dist.all_gather_into_tensor(out, local, group=group)
+        out = gather_tiles(local.cpu(), tiles_pad, group, dst)
+        return None if out is None else out.to(local.device)
+    out = None
+    parts = None
+    if rank == dst:
+        out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        parts = list(out.chunk(world))
+    dist.gather(local, gather_list=parts, dst=dst, group=group)
     return out
 
 
