@@ -37,13 +37,17 @@ def gather_tiles(local, tiles_pad: int, group=None, dst: int = 0):
         # rehearsal path (several ranks on one GPU): gloo gathers host copies
         out = gather_tiles(local.cpu(), tiles_pad, group, dst)
         return None if out is None else out.to(local.device)
-    out = None
-    parts = None
-    if rank == dst:
-        out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                          device=local.device)
-        parts = list(out.chunk(world))
-    dist.gather(local, gather_list=parts, dst=dst, group=group)
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device) if rank == dst else None
+    try:
+        dist.gather(local, gather_list=list(out.chunk(world)) if out is not None else None,
+                    dst=dst, group=group)
+    except NotImplementedError:
+        # a backend without gather refuses it up front on every rank: all-gather instead
+        full = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
+                           dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(full, local, group=group)
+        return full if rank == dst else None
     return out
 
 
