@@ -10,6 +10,7 @@ rays grazing a member where it touches its box.
 import numpy as np
 import pytest
 
+from vulkancomputeraytracing_amd import _native as N
 from vulkancomputeraytracing_amd import scene as S
 
 f32 = np.float32
@@ -329,3 +330,91 @@ def test_hierarchy_is_aligned():
             dd = np.concatenate(out)
             return dd[dd > 0]
         assert np.median(diag(t["node"])) <= 4 * np.median(diag(t["bound"]))
+
+
+def member_hb_cc_disc(t, o, d):
+    """member_disc's fp32 hb, cc and disc (tracer.hip pair_disc_cc)."""
+    g = t["geom"][t["nbig"]:]
+    cx = np.stack([g[:, 0], g[:, 1], g[:, 8], g[:, 9]], 1)
+    cy = np.stack([g[:, 2], g[:, 3], g[:, 10], g[:, 11]], 1)
+    cz = np.stack([g[:, 4], g[:, 5], g[:, 12], g[:, 13]], 1)
+    r2 = np.stack([g[:, 6], g[:, 7], g[:, 14], g[:, 15]], 1)
+    a = ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])[:, None, None]
+    ox, oy, oz = (o[:, k, None, None] for k in range(3))
+    dx, dy, dz = (d[:, k, None, None] for k in range(3))
+    ocx, ocy, ocz = ox - cx[None], oy - cy[None], oz - cz[None]
+    hb = (ocx * dx + ocy * dy) + ocz * dz
+    cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2[None]
+    with np.errstate(over="ignore", invalid="ignore"):
+        return hb, cc, hb * hb - a * cc
+
+
+def camera_rays_f32(cam, px, py, jx, jy):
+    """Camera rays exactly as tracer.hip trace_impl builds them in fp32 (shader.comp:43-52):
+    pc = (p00 + px du) + py dv; ps = pc + (jx du + jy dv); d = ps - centre."""
+    p00, du, dv, ctr = (cam[3 * k:3 * k + 3].astype(f32) for k in range(4))
+    px, py = px.astype(f32)[:, None], py.astype(f32)[:, None]
+    jx, jy = jx.astype(f32)[:, None], jy.astype(f32)[:, None]
+    pc = (p00[None] + px * du[None]) + py * dv[None]
+    ps = pc + (jx * du[None] + jy * dv[None])
+    d = (ps - ctr[None]).astype(f32)
+    o = np.broadcast_to(ctr, d.shape).astype(f32)
+    return o, d
+
+
+@pytest.mark.parametrize("name,w,h,world,rank", [("final", 1920, 1080, 1, 0),
+                                                 ("final", 800, 450, 8, 3),
+                                                 ("final", 160, 90, 1, 0),
+                                                 ("stress4096", 3840, 2160, 1, 0)])
+def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
+    """The flat scan's camera rays start from their tile's group list (csrc/primary.cpp) and
+    skip the hierarchy, so a list must hold every group with a member that may be accepted
+    (disc >= 0 and (hb < 0 or cc < 0), tracer.hip may_hit) for any camera ray of the tile:
+    checked on fp32 emulations of the kernel's rays for every pixel of sampled tiles, at the
+    jitter table's extreme and random samples."""
+    from tests import oracle_py
+    from vulkancomputeraytracing_amd.renderer import RenderDesc, tiles_for_rank
+    o = oracle_py.load()
+    sp = S.builtin_scene(name)
+    t = S.cull_tables(sp)
+    desc = RenderDesc(width=w, height=h, world_size=world, rank=rank)
+    pl = S.primary_lists(sp, desc)
+    cam = o.camera(o.config(w, h, 1, 10))
+    tiles = tiles_for_rank(w, h, world, rank)
+    info = pl["info"]
+    assert len(info) == len(tiles)
+    cnt = info & 15
+    listed = np.nonzero(cnt != 15)[0]
+    assert len(listed) > 0.5 * len(tiles)  # most tiles get a list
+    assert (cnt[listed] <= 8).all()
+    # jitter of the first 1024 samples: -0.5 + rand(i, i), the extremes and a few others
+    lib = N.lib()
+    jit = np.array([[f32(-0.5) + f32(lib.vcrt_canonical_rand(float(i), float(i))),
+                     f32(-0.5) + f32(lib.vcrt_canonical_rand(float(i + 1), float(i + 1)))]
+                    for i in range(1024)], f32)
+    rng = np.random.default_rng(11)
+    pick = [int(np.argmin(jit[:, 0])), int(np.argmax(jit[:, 0])), int(np.argmin(jit[:, 1])),
+            int(np.argmax(jit[:, 1]))] + list(rng.integers(0, 1024, 2))
+    valid = t["index"][t["nbig"]:] >= 0
+    tx_n = (w + 7) // 8
+    sample = rng.choice(listed, size=min(120, len(listed)), replace=False)
+    sample = np.concatenate([sample, listed[:4], listed[-4:]])
+    total_may = control_hits = 0
+    for lt in sample:
+        ty, tx = divmod(tiles[lt], tx_n)
+        ids = pl["ids"][(info[lt] >> 4):(info[lt] >> 4) + cnt[lt]]
+        inlist = np.zeros(valid.shape[0], bool)
+        inlist[ids] = True
+        px = np.repeat(8 * tx + np.arange(64) % 8, len(pick))
+        py = np.repeat(8 * ty + np.arange(64) // 8, len(pick))
+        jj = np.tile(np.array(pick), 64)
+        og, dg = camera_rays_f32(cam, px, py, jit[jj, 0], jit[jj, 1])
+        hb, cc, disc = member_hb_cc_disc(t, og, dg)
+        may = (~(disc < 0)) & ((hb < 0) | (cc < 0)) & valid[None]
+        missing = may & ~inlist[None, :, None]
+        assert not missing.any(), f"tile {tiles[lt]}: {int(missing.sum())} candidates not listed"
+        total_may += int(may.sum())
+        if cnt[lt]:  # control: without its last group the list would miss candidates
+            inlist[ids[-1]] = False
+            control_hits += bool((may & ~inlist[None, :, None]).any())
+    assert total_may > 0 and control_hits > 0.1 * len(sample)

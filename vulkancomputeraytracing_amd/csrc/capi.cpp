@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -72,6 +73,9 @@ struct RendererState {
     float4* d_cbound_nf = nullptr;
     float4* d_cnode = nullptr;
     float4* d_ctop = nullptr;
+    uint32_t* d_prim_info = nullptr;  // camera-ray tile lists (primary.cpp), flat scan only
+    uint16_t* d_prim_ids = nullptr;
+    bool primary_lists = true;        // VCRT_PRIMARY_LISTS=0 turns them off
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
     uint32_t total_pixels = 0, total_items = 0;
@@ -160,6 +164,18 @@ std::string library_dir() {
     return ".";
 }
 
+// pixel00, delta_u, delta_v, centre: TraceParams.cam
+std::array<float, 12> camera_array() {
+    const vcrt::f3 v[4] = {g.cam.pixel00, g.cam.delta_u, g.cam.delta_v, g.cam.center};
+    std::array<float, 12> c{};
+    for (int i = 0; i < 4; i++) {
+        c[3 * i + 0] = v[i].x;
+        c[3 * i + 1] = v[i].y;
+        c[3 * i + 2] = v[i].z;
+    }
+    return c;
+}
+
 void free_scene() {
     if (g.d_geom) (void)hipFree(g.d_geom);
     if (g.d_center_radius) (void)hipFree(g.d_center_radius);
@@ -174,6 +190,10 @@ void free_scene() {
     if (g.d_cbound_nf) (void)hipFree(g.d_cbound_nf);
     if (g.d_cnode) (void)hipFree(g.d_cnode);
     if (g.d_ctop) (void)hipFree(g.d_ctop);
+    if (g.d_prim_info) (void)hipFree(g.d_prim_info);
+    if (g.d_prim_ids) (void)hipFree(g.d_prim_ids);
+    g.d_prim_info = nullptr;
+    g.d_prim_ids = nullptr;
     g.d_cgroup = nullptr;
     g.d_cbound = nullptr;
     g.d_cbound_nf = nullptr;
@@ -403,6 +423,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
     if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VCRT_PRIMARY_LISTS")) g.primary_lists = std::atoi(e) != 0;
     if (const char* e = std::getenv("VCRT_CULL_LANE_TABLES"))
         g.cull_lane_tables = std::strcmp(e, "lds") == 0 ? 1 : std::strcmp(e, "global") == 0 ? 2 : 0;
     // Blocks run from the last local tile to the first: the bottom of the frame (ground and
@@ -487,6 +508,19 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         g.ncgroups = ct.ngroups;
         g.ncbig = ct.nbig;
         std::memcpy(g.cmargin, ct.margin, sizeof(ct.margin));
+        if (g.primary_lists && g.local_tiles > 0) {
+            // camera rays of a tile start from its group list (primary.cpp)
+            vcrt::PrimaryLists pl;
+            vcrt::build_primary_lists(ct, camera_array().data(), g.desc.width, g.desc.height,
+                                      g.desc.rank, g.desc.world_size, pl);
+            VCRT_TRY(hipMalloc(&g.d_prim_info, sizeof(uint32_t) * pl.info.size()));
+            VCRT_TRY(hipMemcpy(g.d_prim_info, pl.info.data(), sizeof(uint32_t) * pl.info.size(),
+                               hipMemcpyHostToDevice));
+            VCRT_TRY(hipMalloc(&g.d_prim_ids, sizeof(uint16_t) * (pl.ids.size() + 1)));
+            if (!pl.ids.empty())
+                VCRT_TRY(hipMemcpy(g.d_prim_ids, pl.ids.data(), sizeof(uint16_t) * pl.ids.size(),
+                                   hipMemcpyHostToDevice));
+        }
     }
     VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float) * table.size()));
     VCRT_TRY(hipMemcpy(g.d_geom, table.data(), sizeof(float) * table.size(),
@@ -556,6 +590,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.cbound_nf = g.d_cbound_nf;
         p.cnode = g.d_cnode;
         p.ctop = g.d_ctop;
+        p.prim_info = g.d_prim_info;
+        p.prim_ids = g.d_prim_ids;
         p.ncgroups = g.ncgroups;
         p.nbig = g.ncbig;
         for (int k = 0; k < 4; k++) p.box_margin[k] = g.cmargin[k];
@@ -573,12 +609,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.nchunks = g.nchunks;
         p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
                   (slab ? vcrt::kFlagSlab : 0u);
-        const vcrt::f3 v[4] = {g.cam.pixel00, g.cam.delta_u, g.cam.delta_v, g.cam.center};
-        for (int i = 0; i < 4; i++) {
-            p.cam[3 * i + 0] = v[i].x;
-            p.cam[3 * i + 1] = v[i].y;
-            p.cam[3 * i + 2] = v[i].z;
-        }
+        const std::array<float, 12> cam = camera_array();
+        for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
         // scan table: (groups + 1 padding group) x 64 B
         const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
         // per-lane culled scan: tables in LDS. Up to 32 KB with 256-thread workgroups (5 per
@@ -890,6 +922,34 @@ int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom,
         if (index) std::memcpy(index, ct.index.data(), sizeof(int32_t) * ct.index.size());
     }
     return ct.ngroups;
+}
+
+int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt_render_desc* desc,
+                           uint32_t* info, int32_t cap_tiles, uint16_t* ids, int32_t cap_ids) {
+    if (!desc || !desc_valid(*desc) || count < 0 || (count > 0 && !spheres)) return -1;
+    vcrt::CullTables ct;
+    if (!vcrt::build_cull_tables(spheres, count, ct)) return -1;
+    const vcrt_camera& c = desc->camera;
+    const vcrt::Camera cm = vcrt::make_camera(desc->width, desc->height,
+                                              vcrt::mk(c.lookfrom[0], c.lookfrom[1], c.lookfrom[2]),
+                                              vcrt::mk(c.lookat[0], c.lookat[1], c.lookat[2]),
+                                              vcrt::mk(c.vup[0], c.vup[1], c.vup[2]), c.vfov,
+                                              [](double x) { return std::tan(x); });
+    const vcrt::f3 v[4] = {cm.pixel00, cm.delta_u, cm.delta_v, cm.center};
+    float cam[12];
+    for (int i = 0; i < 4; i++) {
+        cam[3 * i + 0] = v[i].x;
+        cam[3 * i + 1] = v[i].y;
+        cam[3 * i + 2] = v[i].z;
+    }
+    vcrt::PrimaryLists pl;
+    vcrt::build_primary_lists(ct, cam, desc->width, desc->height, desc->rank, desc->world_size,
+                              pl);
+    if (info && cap_tiles >= static_cast<int32_t>(pl.info.size()))
+        std::memcpy(info, pl.info.data(), sizeof(uint32_t) * pl.info.size());
+    if (ids && cap_ids >= static_cast<int32_t>(pl.ids.size()))
+        std::memcpy(ids, pl.ids.data(), sizeof(uint16_t) * pl.ids.size());
+    return static_cast<int32_t>(pl.ids.size());
 }
 
 float vcrt_canonical_sin(float x) { return vcrt::sin_canonical(x); }

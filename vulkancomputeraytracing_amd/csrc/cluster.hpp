@@ -33,4 +33,20 @@ struct CullTables {
 // than 16 spheres or any centre/radius outside +-2^30 (or not finite).
 bool build_cull_tables(const vcrt_sphere* spheres, int32_t count, CullTables& out);
 
+// Primary-ray tile lists (the flat scan's camera rays skip the node level): for every local
+// 8x8 tile, the hierarchy groups a camera ray through the tile may need, by a conservative
+// pyramid-box test in double (primary.cpp). info[lt] = offset << 4 | count, count <= 8, or
+// kPrimaryNone (that tile's camera rays take the hierarchy like any other ray).
+constexpr uint32_t kPrimaryMax = 8;
+constexpr uint32_t kPrimaryNone = 15;
+
+struct PrimaryLists {
+    std::vector<uint32_t> info;  // [local tiles]
+    std::vector<uint16_t> ids;   // hierarchy group indices, by tile
+};
+
+// cam: pixel00, delta_u, delta_v, centre (shader.comp:18-43) as the kernels get them.
+void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
+                         int32_t height, int32_t rank, int32_t world, PrimaryLists& out);
+
 }  // namespace vcrt

@@ -1,0 +1,148 @@
+// primary.cpp -- per-tile group lists for camera rays (the flat culled scan's primary segments).
+//
+// A camera ray of pixel (x, y) and sample i (shader.comp:43-52) starts at the camera centre and
+// points at pixel00 + (x + jx) delta_u + (y + jy) delta_v with the jitter (jx, jy) in
+// [-0.5, 0.5). All camera rays of an 8x8 tile therefore lie in the pyramid from the centre
+// through the tile's footprint grown by half a pixel: the rectangle R of the image plane. The
+// kernel evaluates that direction in fp32 (a few roundings: |error| < 1e-5 of the scene size
+// here), so R is grown by a further 1e-3 world units.
+//
+// Which groups may such a ray need? A member with fp32 discriminant >= 0 whose root can be
+// accepted (tracer.hip may_hit: hb < 0 or cc < 0) has its centre within r + M_s of the ray
+// line (margin argument, tracer.hip fact (2)), and the closest line point lies at t >= 0 up to
+// the rounding of hb (< 1e-5 here) or the camera lies inside the sphere. So the member's box,
+// grown by the box margin M_b = K_b Q (Q = (|o| + c_max)^2 + r_max^2 with o = the camera) and
+// by 1e-3, meets the pyramid. The test below keeps every box that no side plane of the pyramid
+// separates from it (conservative: it ignores the other separating axes), for chunks, then
+// their nodes, then their groups (a node's box and margin cover its groups' grown boxes).
+// Tiles with more than kPrimaryMax groups get no list. tests/test_cull_cpu.py checks the lists
+// against fp32 emulations of the kernel's camera rays and discriminants.
+#include <algorithm>
+#include <cmath>
+
+#include "cluster.hpp"
+#include "vcrt_math.h"
+
+namespace vcrt {
+namespace {
+
+struct DBox {
+    double c[3], h[3];  // centre, half extent (grown)
+    bool always = false;
+};
+
+// Element i of a pair-SoA box table, grown by its margin K * Q and `extra`.
+DBox grown_box(const std::vector<float>& table, size_t i, double Q, double extra) {
+    const float* t = &table[(i / 2) * 16];
+    const int e = static_cast<int>(i % 2);
+    DBox b;
+    const double K = t[12 + e];
+    const double g = K * Q * (1.0 + 1e-6) + extra;
+    b.always = !(g < 1e30);  // K = inf: a zero radius, never ruled out
+    for (int a = 0; a < 3; a++) {
+        const double lo = t[2 * a + e], hi = t[6 + 2 * a + e];
+        b.c[a] = 0.5 * (lo + hi);
+        b.h[a] = 0.5 * (hi - lo) + g;
+    }
+    return b;
+}
+
+struct Pyramid {
+    double apex[3];
+    double n[4][3];  // inward side-plane normals
+};
+
+bool outside(const Pyramid& P, const DBox& b) {
+    if (b.always) return false;
+    for (int k = 0; k < 4; k++) {
+        double s = 0.0, r = 0.0;
+        for (int a = 0; a < 3; a++) {
+            s += P.n[k][a] * (b.c[a] - P.apex[a]);
+            r += std::fabs(P.n[k][a]) * b.h[a];
+        }
+        if (s + r < 0.0) return true;
+    }
+    return false;
+}
+
+}  // namespace
+
+void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
+                         int32_t height, int32_t rank, int32_t world, PrimaryLists& out) {
+    out.info.clear();
+    out.ids.clear();
+    const uint32_t tiles_x = static_cast<uint32_t>((width + 7) / 8);
+    const uint32_t tiles_y = static_cast<uint32_t>((height + 7) / 8);
+    double p00[3], du[3], dv[3], o[3];
+    for (int a = 0; a < 3; a++) {
+        p00[a] = cam[a];
+        du[a] = cam[3 + a];
+        dv[a] = cam[6 + a];
+        o[a] = cam[9 + a];
+    }
+    const double on = std::sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+    const double Q = (on + ct.margin[0]) * (on + ct.margin[0]) + ct.margin[1];
+    const double ndu = std::sqrt(du[0] * du[0] + du[1] * du[1] + du[2] * du[2]);
+    const double ndv = std::sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+    const double kExtra = 1e-3;
+    const size_t ng = static_cast<size_t>(ct.ngroups);
+    std::vector<DBox> gb(ng), nb(ng / kNodeGroups), tb((ng + 63) / 64);
+    for (size_t i = 0; i < gb.size(); i++) gb[i] = grown_box(ct.bound, i, Q, kExtra);
+    for (size_t i = 0; i < nb.size(); i++) nb[i] = grown_box(ct.node, i, Q, kExtra);
+    for (size_t i = 0; i < tb.size(); i++) tb[i] = grown_box(ct.top, i, Q, kExtra);
+    std::vector<bool> real(ng, false);
+    for (size_t i = 0; i < ng; i++)
+        for (int k = 0; k < 4; k++) real[i] = real[i] || ct.index[(ct.nbig + i) * 4 + k] >= 0;
+    // local tiles in the kernel's order (vcrt_math.h tile_of)
+    uint32_t nloc = 0;
+    for (uint32_t ty = 0; ty < tiles_y; ty++)
+        for (uint32_t tx = 0; tx < tiles_x; tx++)
+            if ((tx + ty) % static_cast<uint32_t>(world) == static_cast<uint32_t>(rank)) nloc++;
+    out.info.assign(nloc, kPrimaryNone);
+    uint32_t found[kPrimaryMax];
+    for (uint32_t lt = 0; lt < nloc; lt++) {
+        uint32_t tx, ty;
+        tile_of(lt, static_cast<uint32_t>(rank), static_cast<uint32_t>(world), tiles_x, &tx, &ty);
+        // the footprint of the tile's sample points, grown by kExtra in the image plane
+        const double X0 = 8.0 * tx - 0.5 - kExtra / ndu, X1 = 8.0 * tx + 7.5 + kExtra / ndu;
+        const double Y0 = 8.0 * ty - 0.5 - kExtra / ndv, Y1 = 8.0 * ty + 7.5 + kExtra / ndv;
+        const double XY[4][2] = {{X0, Y0}, {X1, Y0}, {X1, Y1}, {X0, Y1}};
+        double D[4][3], mid[3] = {0, 0, 0};
+        for (int k = 0; k < 4; k++)
+            for (int a = 0; a < 3; a++) {
+                D[k][a] = p00[a] + XY[k][0] * du[a] + XY[k][1] * dv[a] - o[a];
+                mid[a] += 0.25 * D[k][a];
+            }
+        Pyramid P;
+        for (int a = 0; a < 3; a++) P.apex[a] = o[a];
+        for (int k = 0; k < 4; k++) {
+            const double* u = D[k];
+            const double* v = D[(k + 1) % 4];
+            double n[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2],
+                           u[0] * v[1] - u[1] * v[0]};
+            const double s = n[0] * mid[0] + n[1] * mid[1] + n[2] * mid[2];
+            for (int a = 0; a < 3; a++) P.n[k][a] = s < 0.0 ? -n[a] : n[a];
+        }
+        uint32_t cnt = 0;
+        bool over = false;
+        for (size_t ci = 0; ci < tb.size() && !over; ci++) {
+            if (outside(P, tb[ci])) continue;
+            for (size_t ni = ci * 8; ni < std::min(nb.size(), ci * 8 + 8) && !over; ni++) {
+                if (outside(P, nb[ni])) continue;
+                for (size_t gi = ni * kNodeGroups; gi < ni * kNodeGroups + kNodeGroups; gi++) {
+                    if (!real[gi] || outside(P, gb[gi])) continue;
+                    if (cnt == kPrimaryMax) {
+                        over = true;
+                        break;
+                    }
+                    found[cnt++] = static_cast<uint32_t>(gi);
+                }
+            }
+        }
+        if (over) continue;
+        out.info[lt] = static_cast<uint32_t>(out.ids.size()) << 4 | cnt;
+        for (uint32_t k = 0; k < cnt; k++) out.ids.push_back(static_cast<uint16_t>(found[k]));
+    }
+}
+
+}  // namespace vcrt

@@ -779,7 +779,8 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
 template <bool kStats, bool kWide>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
                                                  const float4* tgroup, WaveScratch<kWide>* ws,
-                                                 const f3 o, const f3 d, float& max_t, int& best,
+                                                 const f3 o, const f3 d, bool primary,
+                                                 uint32_t lt, float& max_t, int& best,
                                                  uint64_t& groups_tested, uint64_t& bounds_tested,
                                                  PhaseTicks& pt) {
     uint64_t t_in = 0;
@@ -811,6 +812,26 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     const uint32_t nact = (uint32_t)__popcll(live), rank = lanes_below(live);
     ws->key[lane] = pack_hit(max_t, best);
     FlatStacks h = {0u, 0u, 0u};
+    // A camera ray (primary) whose tile has a group list (primary.cpp) pushes those groups
+    // straight onto the group stack and skips the chunk and node levels: the list holds every
+    // group such a ray may need (at most 8 per lane: at most 512 entries on the empty stack).
+    bool listed = false;
+    uint32_t lcnt = 0u, loff = 0u;
+    if (primary && p.prim_info != nullptr) {
+        const uint32_t inf = p.prim_info[lt];
+        listed = (inf & 15u) != 15u;
+        lcnt = listed ? inf & 15u : 0u;
+        loff = inf >> 4;
+    }
+    if (__ballot(lcnt != 0u)) {  // the stack height stays wave-uniform: prefix over all lanes
+        uint32_t tot;
+        uint32_t pos = wave_prefix<4>(lcnt, tot);
+        h.group = tot;
+        const uint16_t* ids = p.prim_ids + loff;
+        for (uint32_t k = 0; k < lcnt; ++k)
+            ws->group[pos++] =
+                (typename FlatFmt<kWide>::entry_t)((lane << FlatFmt<kWide>::kShift) | ids[k]);
+    }
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* top = (cfloat4*)p.ctop;
     const int ncg = p.ncgroups;
@@ -827,7 +848,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                 tops = ~push_bound_pair(0u, br, tp.b0, tp.b1, tp.b2, tp.b3) & 3u;
                 n_bounds += 2;
             }
-            const bool in_chunk = ((tops >> ((base >> 6) & 1)) & 1u) != 0;
+            const bool in_chunk = !listed && ((tops >> ((base >> 6) & 1)) & 1u) != 0;
             if (__ballot(in_chunk) == 0) continue;
             // level 1, wave-uniform: nodes of this chunk, per-lane bits -> node entries
             const int nn = min(8, (ncg - base) >> 3);
@@ -1137,8 +1158,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kCull == 4 || kCull == 5)
-                    scan_culled_flat<kStats, kWide>(p, tbound, tgroup, ws, o, d, max_t, best, w_groups,
-                                             w_bounds, pt);
+                    scan_culled_flat<kStats, kWide>(p, tbound, tgroup, ws, o, d, pass == 0,
+                                                    q >> 6, max_t, best, w_groups, w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);

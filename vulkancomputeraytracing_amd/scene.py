@@ -90,3 +90,24 @@ def cull_tables(spheres: np.ndarray) -> dict | None:
     assert got == g
     return {"nbig": nb, "geom": geom, "bound": bound, "node": node, "top": top, "index": index,
             "margin": margin}
+
+
+def primary_lists(spheres: np.ndarray, desc) -> dict | None:
+    """The flat scan's camera-ray tile lists (host computation, no GPU; csrc/primary.cpp) for
+    `spheres` and a RenderDesc: ``info`` [local tiles] uint32 (offset << 4 | count, count 15 =
+    no list) and ``ids`` uint16 hierarchy group indices. None without culling tables."""
+    spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+    lib = N.lib()
+    d = desc.to_c()
+    n = lib.vcrt_primary_lists(spheres.ctypes.data, len(spheres), ctypes.byref(d), None, 0,
+                               None, 0)
+    if n < 0:
+        return None
+    from .renderer import tiles_for_rank
+    nt = len(tiles_for_rank(desc.width, desc.height, desc.world_size, desc.rank))
+    info = np.zeros(nt, np.uint32)
+    ids = np.zeros(max(n, 1), np.uint16)
+    got = lib.vcrt_primary_lists(spheres.ctypes.data, len(spheres), ctypes.byref(d),
+                                 info.ctypes.data, nt, ids.ctypes.data, len(ids))
+    assert got == n
+    return {"info": info, "ids": ids[:n]}
