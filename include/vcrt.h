@@ -199,11 +199,12 @@ int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom,
                          float* node, float* top, int32_t* index, int32_t* big_groups,
                          float* margin4, int32_t cap_groups);
 
-/* The flat culled scan's camera-ray tile lists for a scene and render description (host only,
- * no GPU; csrc/primary.cpp): for each local tile of desc->rank (in the kernels' local-tile
- * order), info = offset << 4 | count of its hierarchy groups in ids (count <= 8), or 15 when
- * the tile has no list. Returns the number of ids (-1: no culling tables, or an invalid desc),
- * and writes info / ids when cap_tiles / cap_ids are large enough (pointers may be NULL). */
+/* The flat culled scan's camera-ray lists for a scene and render description (host only, no
+ * GPU; csrc/primary.cpp): for each 4x4-pixel quarter (qx, qy) of each local tile lt of
+ * desc->rank (in the kernels' local-tile order), info[4 lt + 2 qy + qx] = offset << 4 | count
+ * of its hierarchy groups in ids (count <= 8), or 15 when it has no list. Returns the number of
+ * ids (-1: no culling tables, or an invalid desc), and writes info / ids when cap_tiles (entries
+ * of info) / cap_ids are large enough (pointers may be NULL). */
 int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt_render_desc* desc,
                            uint32_t* info, int32_t cap_tiles, uint16_t* ids, int32_t cap_ids);
 

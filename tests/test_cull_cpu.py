@@ -367,11 +367,11 @@ def camera_rays_f32(cam, px, py, jx, jy):
                                                  ("final", 160, 90, 1, 0),
                                                  ("stress4096", 3840, 2160, 1, 0)])
 def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
-    """The flat scan's camera rays start from their tile's group list (csrc/primary.cpp) and
-    skip the hierarchy, so a list must hold every group with a member that may be accepted
-    (disc >= 0 and (hb < 0 or cc < 0), tracer.hip may_hit) for any camera ray of the tile:
-    checked on fp32 emulations of the kernel's rays for every pixel of sampled tiles, at the
-    jitter table's extreme and random samples."""
+    """The flat scan's camera rays start from the group list of their 4x4-pixel quarter of a
+    tile (csrc/primary.cpp) and skip the hierarchy, so a list must hold every group with a
+    member that may be accepted (disc >= 0 and (hb < 0 or cc < 0), tracer.hip may_hit) for any
+    camera ray of the quarter: checked on fp32 emulations of the kernel's rays for every pixel
+    of sampled quarters, at the jitter table's extreme and random samples."""
     from tests import oracle_py
     from vulkancomputeraytracing_amd.renderer import RenderDesc, tiles_for_rank
     o = oracle_py.load()
@@ -382,10 +382,10 @@ def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
     cam = o.camera(o.config(w, h, 1, 10))
     tiles = tiles_for_rank(w, h, world, rank)
     info = pl["info"]
-    assert len(info) == len(tiles)
+    assert len(info) == 4 * len(tiles)
     cnt = info & 15
     listed = np.nonzero(cnt != 15)[0]
-    assert len(listed) > 0.5 * len(tiles)  # most tiles get a list
+    assert len(listed) > 0.5 * len(info)  # most quarters get a list
     assert (cnt[listed] <= 8).all()
     # jitter of the first 1024 samples: -0.5 + rand(i, i), the extremes and a few others
     lib = N.lib()
@@ -397,24 +397,25 @@ def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
             int(np.argmax(jit[:, 1]))] + list(rng.integers(0, 1024, 2))
     valid = t["index"][t["nbig"]:] >= 0
     tx_n = (w + 7) // 8
-    sample = rng.choice(listed, size=min(120, len(listed)), replace=False)
+    sample = rng.choice(listed, size=min(160, len(listed)), replace=False)
     sample = np.concatenate([sample, listed[:4], listed[-4:]])
     total_may = control_hits = 0
-    for lt in sample:
-        ty, tx = divmod(tiles[lt], tx_n)
-        ids = pl["ids"][(info[lt] >> 4):(info[lt] >> 4) + cnt[lt]]
+    for e in sample:
+        ty, tx = divmod(tiles[e >> 2], tx_n)
+        qx, qy = e & 1, (e >> 1) & 1
+        ids = pl["ids"][(info[e] >> 4):(info[e] >> 4) + cnt[e]]
         inlist = np.zeros(valid.shape[0], bool)
         inlist[ids] = True
-        px = np.repeat(8 * tx + np.arange(64) % 8, len(pick))
-        py = np.repeat(8 * ty + np.arange(64) // 8, len(pick))
-        jj = np.tile(np.array(pick), 64)
+        px = np.repeat(8 * tx + 4 * qx + np.arange(16) % 4, len(pick))
+        py = np.repeat(8 * ty + 4 * qy + np.arange(16) // 4, len(pick))
+        jj = np.tile(np.array(pick), 16)
         og, dg = camera_rays_f32(cam, px, py, jit[jj, 0], jit[jj, 1])
         hb, cc, disc = member_hb_cc_disc(t, og, dg)
         may = (~(disc < 0)) & ((hb < 0) | (cc < 0)) & valid[None]
         missing = may & ~inlist[None, :, None]
-        assert not missing.any(), f"tile {tiles[lt]}: {int(missing.sum())} candidates not listed"
+        assert not missing.any(), f"entry {e}: {int(missing.sum())} candidates not listed"
         total_may += int(may.sum())
-        if cnt[lt]:  # control: without its last group the list would miss candidates
+        if cnt[e]:  # control: without its last group the list would miss candidates
             inlist[ids[-1]] = False
             control_hits += bool((may & ~inlist[None, :, None]).any())
     assert total_may > 0 and control_hits > 0.1 * len(sample)

@@ -33,15 +33,15 @@ struct CullTables {
 // than 16 spheres or any centre/radius outside +-2^30 (or not finite).
 bool build_cull_tables(const vcrt_sphere* spheres, int32_t count, CullTables& out);
 
-// Primary-ray tile lists (the flat scan's camera rays skip the node level): for every local
-// 8x8 tile, the hierarchy groups a camera ray through the tile may need, by a conservative
-// pyramid-box test in double (primary.cpp). info[lt] = offset << 4 | count, count <= 8, or
-// kPrimaryNone (that tile's camera rays take the hierarchy like any other ray).
+// Primary-ray lists (the flat scan's camera rays skip the node level): for every 4x4-pixel
+// quarter of every local 8x8 tile, the hierarchy groups a camera ray through it may need, by a
+// conservative pyramid-box test in double (primary.cpp). info[4 lt + 2 qy + qx] =
+// offset << 4 | count, count <= 8, or kPrimaryNone (those camera rays take the hierarchy).
 constexpr uint32_t kPrimaryMax = 8;
 constexpr uint32_t kPrimaryNone = 15;
 
 struct PrimaryLists {
-    std::vector<uint32_t> info;  // [local tiles]
+    std::vector<uint32_t> info;  // [4 x local tiles]
     std::vector<uint16_t> ids;   // hierarchy group indices, by tile
 };
 

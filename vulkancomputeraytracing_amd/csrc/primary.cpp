@@ -2,8 +2,9 @@
 //
 // A camera ray of pixel (x, y) and sample i (shader.comp:43-52) starts at the camera centre and
 // points at pixel00 + (x + jx) delta_u + (y + jy) delta_v with the jitter (jx, jy) in
-// [-0.5, 0.5). All camera rays of an 8x8 tile therefore lie in the pyramid from the centre
-// through the tile's footprint grown by half a pixel: the rectangle R of the image plane. The
+// [-0.5, 0.5). All camera rays of a 4x4-pixel quarter of a tile therefore lie in the pyramid
+// from the centre through the quarter's footprint grown by half a pixel: the rectangle R of the
+// image plane. The
 // kernel evaluates that direction in fp32 (a few roundings: |error| < 1e-5 of the scene size
 // here), so R is grown by a further 1e-3 world units.
 //
@@ -98,14 +99,17 @@ void build_primary_lists(const CullTables& ct, const float cam[12], int32_t widt
     for (uint32_t ty = 0; ty < tiles_y; ty++)
         for (uint32_t tx = 0; tx < tiles_x; tx++)
             if ((tx + ty) % static_cast<uint32_t>(world) == static_cast<uint32_t>(rank)) nloc++;
-    out.info.assign(nloc, kPrimaryNone);
+    out.info.assign(4 * nloc, kPrimaryNone);
     uint32_t found[kPrimaryMax];
-    for (uint32_t lt = 0; lt < nloc; lt++) {
+    for (uint32_t e = 0; e < 4 * nloc; e++) {
+        // entry 4 lt + 2 qy + qx: the 4x4-pixel quarter (qx, qy) of local tile lt
+        const uint32_t lt = e >> 2, qx = e & 1u, qy = (e >> 1) & 1u;
         uint32_t tx, ty;
         tile_of(lt, static_cast<uint32_t>(rank), static_cast<uint32_t>(world), tiles_x, &tx, &ty);
-        // the footprint of the tile's sample points, grown by kExtra in the image plane
-        const double X0 = 8.0 * tx - 0.5 - kExtra / ndu, X1 = 8.0 * tx + 7.5 + kExtra / ndu;
-        const double Y0 = 8.0 * ty - 0.5 - kExtra / ndv, Y1 = 8.0 * ty + 7.5 + kExtra / ndv;
+        // the footprint of the quarter's sample points, grown by kExtra in the image plane
+        const double x0 = 8.0 * tx + 4.0 * qx, y0 = 8.0 * ty + 4.0 * qy;
+        const double X0 = x0 - 0.5 - kExtra / ndu, X1 = x0 + 3.5 + kExtra / ndu;
+        const double Y0 = y0 - 0.5 - kExtra / ndv, Y1 = y0 + 3.5 + kExtra / ndv;
         const double XY[4][2] = {{X0, Y0}, {X1, Y0}, {X1, Y1}, {X0, Y1}};
         double D[4][3], mid[3] = {0, 0, 0};
         for (int k = 0; k < 4; k++)
@@ -140,7 +144,7 @@ void build_primary_lists(const CullTables& ct, const float cam[12], int32_t widt
             }
         }
         if (over) continue;
-        out.info[lt] = static_cast<uint32_t>(out.ids.size()) << 4 | cnt;
+        out.info[e] = static_cast<uint32_t>(out.ids.size()) << 4 | cnt;
         for (uint32_t k = 0; k < cnt; k++) out.ids.push_back(static_cast<uint16_t>(found[k]));
     }
 }

@@ -780,7 +780,7 @@ template <bool kStats, bool kWide>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
                                                  const float4* tgroup, WaveScratch<kWide>* ws,
                                                  const f3 o, const f3 d, bool primary,
-                                                 uint32_t lt, float& max_t, int& best,
+                                                 uint32_t item, float& max_t, int& best,
                                                  uint64_t& groups_tested, uint64_t& bounds_tested,
                                                  PhaseTicks& pt) {
     uint64_t t_in = 0;
@@ -818,7 +818,9 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     bool listed = false;
     uint32_t lcnt = 0u, loff = 0u;
     if (primary && p.prim_info != nullptr) {
-        const uint32_t inf = p.prim_info[lt];
+        // the list of the item's 4x4 quarter of its tile (slot = 8 y + x)
+        const uint32_t inf =
+            p.prim_info[(item >> 6) * 4u + (((item >> 5) & 1u) << 1) + ((item >> 2) & 1u)];
         listed = (inf & 15u) != 15u;
         lcnt = listed ? inf & 15u : 0u;
         loff = inf >> 4;
@@ -1158,8 +1160,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kCull == 4 || kCull == 5)
-                    scan_culled_flat<kStats, kWide>(p, tbound, tgroup, ws, o, d, pass == 0,
-                                                    q >> 6, max_t, best, w_groups, w_bounds, pt);
+                    scan_culled_flat<kStats, kWide>(p, tbound, tgroup, ws, o, d, pass == 0, q,
+                                                    max_t, best, w_groups, w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);

@@ -44,8 +44,9 @@ struct TraceParams {
                               //   x then y then z, then (K0,K1) -- 80 B per pair
     const float4* cnode;    // [ncgroups / 16 * 4] boxes of node pairs (8 groups per node)
     const float4* ctop;     // boxes of pairs of 64-group chunks, same form
-    const uint32_t* prim_info;  // [local_tiles] camera-ray group list of each local tile:
-                                //   offset << 4 | count (count <= 8; 15 = none), or null
+    const uint32_t* prim_info;  // [4 local_tiles] camera-ray group list of each 4x4 quarter
+                                //   (4 lt + 2 qy + qx) of each local tile: offset << 4 |
+                                //   count (count <= 8; 15 = none), or null
     const uint16_t* prim_ids;   // hierarchy group indices of those lists
     float box_margin[4];    // max |centre|, r_max^2, max |box coordinate|, 0 (rounded up)
     int32_t ncgroups;       // hierarchy groups, multiple of 16

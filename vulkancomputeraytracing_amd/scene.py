@@ -93,9 +93,10 @@ def cull_tables(spheres: np.ndarray) -> dict | None:
 
 
 def primary_lists(spheres: np.ndarray, desc) -> dict | None:
-    """The flat scan's camera-ray tile lists (host computation, no GPU; csrc/primary.cpp) for
-    `spheres` and a RenderDesc: ``info`` [local tiles] uint32 (offset << 4 | count, count 15 =
-    no list) and ``ids`` uint16 hierarchy group indices. None without culling tables."""
+    """The flat scan's camera-ray lists (host computation, no GPU; csrc/primary.cpp) for
+    `spheres` and a RenderDesc: ``info`` [4 x local tiles] uint32, entry 4 lt + 2 qy + qx for the
+    4x4-pixel quarter (qx, qy) of local tile lt (offset << 4 | count, count 15 = no list), and
+    ``ids`` uint16 hierarchy group indices. None without culling tables."""
     spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
     lib = N.lib()
     d = desc.to_c()
@@ -104,7 +105,7 @@ def primary_lists(spheres: np.ndarray, desc) -> dict | None:
     if n < 0:
         return None
     from .renderer import tiles_for_rank
-    nt = len(tiles_for_rank(desc.width, desc.height, desc.world_size, desc.rank))
+    nt = 4 * len(tiles_for_rank(desc.width, desc.height, desc.world_size, desc.rank))
     info = np.zeros(nt, np.uint32)
     ids = np.zeros(max(n, 1), np.uint16)
     got = lib.vcrt_primary_lists(spheres.ctypes.data, len(spheres), ctypes.byref(d),
