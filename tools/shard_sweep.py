@@ -1,5 +1,5 @@
-"""Per-rank kernel time of an N-way tile-sharded frame, all ranks rendered one after another on
-this GPU: max over ranks is what strong scaling sees; sum vs the unsharded frame shows the
+"""Per-rank kernel time (second frame) of an N-way tile-sharded frame, all ranks rendered one
+after another on this GPU: max over ranks is what strong scaling sees; sum vs the unsharded frame shows the
 per-rank fixed costs (launch, drain)."""
 import argparse
 import json
@@ -17,7 +17,9 @@ p.add_argument("--variant", type=int, default=0)
 a = p.parse_args()
 base = dict(width=1920, height=1080, samples_per_pixel=a.spp, max_depth=10, device=0,
             accumulate_chunk=a.chunk, kernel_variant=a.variant)
+# steady state: the second frame of each renderer (the first after Begin runs ~5% slower)
 with vc.Renderer(vc.RenderDesc(**base), "final") as r:
+    r.draw_next_frame()
     r.draw_next_frame()
     full = r.stats()["kernel_ms"]
 res = {"full_ms": full, "spp": a.spp, "chunk_arg": a.chunk, "variant": a.variant}
@@ -25,6 +27,7 @@ for world in [int(x) for x in a.worlds.split(",")]:
     per = []
     for rank in range(world):
         with vc.Renderer(vc.RenderDesc(rank=rank, world_size=world, **base), "final") as r:
+            r.draw_next_frame()
             r.draw_next_frame()
             st = r.stats()
             per.append(st["kernel_ms"])
