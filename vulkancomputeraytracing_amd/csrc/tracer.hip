@@ -21,7 +21,9 @@
 //   * The sphere-list scan is either the reference's linear scan (wave-uniform groups through
 //     the scalar cache or LDS) or an exact culled scan over a spatial hierarchy (groups of 4,
 //     nodes of 8 groups, chunks of 64 groups), wave-uniform or per lane on an LDS copy of the
-//     tables; see "Culled scan" below for why it returns the same sphere and t.
+//     tables; see "Culled scan" below for why it returns the same sphere and t. In the flat
+//     culled scan a camera ray starts from its pixel quarter's precomputed group list
+//     (csrc/primary.cpp) instead of the hierarchy.
 //   * Only fp32 add/sub/mul plus correctly rounded div/sqrt, no contraction, in everything
 //     that reaches the image: results are bit-identical to the CPU oracle for the same
 //     accumulation order. No MFMA.
