@@ -787,6 +787,10 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                                                  PhaseTicks& pt) {
     uint64_t t_in = 0;
     if constexpr (kStats) t_in = ticks();
+    // the camera-ray list record, loaded ahead of the big list so its latency overlaps it
+    uint32_t inf = 15u;
+    if (primary && p.prim_info != nullptr)  // the list of the item's 4x4 quarter (slot 8 y + x)
+        inf = p.prim_info[(item >> 6) * 4u + (((item >> 5) & 1u) << 1) + ((item >> 2) & 1u)];
     FlatRay my;
     my.ox = o.x;
     my.oy = o.y;
@@ -817,16 +821,8 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     // A camera ray (primary) whose tile has a group list (primary.cpp) pushes those groups
     // straight onto the group stack and skips the chunk and node levels: the list holds every
     // group such a ray may need (at most 8 per lane: at most 512 entries on the empty stack).
-    bool listed = false;
-    uint32_t lcnt = 0u, loff = 0u;
-    if (primary && p.prim_info != nullptr) {
-        // the list of the item's 4x4 quarter of its tile (slot = 8 y + x)
-        const uint32_t inf =
-            p.prim_info[(item >> 6) * 4u + (((item >> 5) & 1u) << 1) + ((item >> 2) & 1u)];
-        listed = (inf & 15u) != 15u;
-        lcnt = listed ? inf & 15u : 0u;
-        loff = inf >> 4;
-    }
+    const bool listed = (inf & 15u) != 15u;
+    const uint32_t lcnt = listed ? inf & 15u : 0u, loff = inf >> 4;
     if (__ballot(lcnt != 0u)) {  // the stack height stays wave-uniform: prefix over all lanes
         uint32_t tot;
         uint32_t pos = wave_prefix<4>(lcnt, tot);
