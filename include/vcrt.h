@@ -92,7 +92,7 @@ typedef struct vcrt_render_desc {
     int32_t world_size;    /* number of shards (GPUs) */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
-    int32_t accumulate_chunk; /* samples per work item (0 = 16, halved down to 4 while the
+    int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 4 while the
                                  rank has < 2^24 work items). A pixel's samples are summed
                                  in order within a chunk and the chunk sums in chunk order;
                                  >= samples_per_pixel reproduces the reference's sequential

@@ -33,7 +33,7 @@ namespace {
 using vcrt::to_vk;
 
 constexpr size_t kCounterBytes = 256;  // work (u32), segments (u64), work_done[2] (u64), padded
-constexpr int32_t kDefaultChunk = 16;        // samples per work item (upper end)
+constexpr int32_t kDefaultChunk = 64;        // samples per work item (upper end)
 
 struct RendererState {
     bool begun = false;
@@ -106,7 +106,7 @@ RendererState g;
         if (e_ != hipSuccess) return to_vk(e_); \
     } while (0)
 
-// Samples per work item when the caller leaves it to us: 16, halved (down to 4) while the
+// Samples per work item when the caller leaves it to us: 64, halved (down to 4) while the
 // rank's work would be fewer than 2^24 items, so every lane of the persistent grid (~400k
 // lanes on MI355X) still gets ~40 items and the drain at the end stays short. A function of
 // the configuration only, so the summation order does not depend on the device.

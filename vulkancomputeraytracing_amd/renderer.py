@@ -32,7 +32,7 @@ class RenderDesc:
     world_size: int = 1             # shards: rank owns the 8x8 tiles with (tx + ty) % world == rank
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
-    accumulate_chunk: int = 0       # 0 = 16; >= spp: the reference's sequential order
+    accumulate_chunk: int = 0       # 0 = 64 (halved for small jobs); >= spp: sequential order
     progressive: bool = False       # frame f continues the sample sequence; average of all frames
     code_object_path: str | None = None
     _path_keepalive: bytes | None = field(default=None, repr=False)
@@ -58,7 +58,7 @@ class RenderDesc:
         return d
 
 
-DEFAULT_ACCUMULATE_CHUNK = 16
+DEFAULT_ACCUMULATE_CHUNK = 64
 
 
 def effective_chunk(spp: int, accumulate_chunk: int = 0, pixels: int | None = None) -> int:
