@@ -136,6 +136,9 @@ typedef struct vcrt_stats {
 vcrt_result vcrt_default_desc(vcrt_render_desc* desc);
 
 vcrt_result vcrt_begin(const vcrt_render_desc* desc);
+/* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
+ * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final
+ * scene at 1080p, ~0.4 s for 4100 spheres at 4K). vcrt_begin sets the final scene. */
 vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count);
 vcrt_result vcrt_draw_next_frame(void);
 vcrt_result vcrt_end(void);
