@@ -472,3 +472,15 @@ def test_bench_multirank_gather_bitwise():
     res = json.loads(line)
     assert res["n_gpus"] == 3
     assert res["validated_bitwise_vs_1gpu"] is True
+
+
+def test_rccl_gather_path_world1():
+    """distributed.gather_tiles on the nccl (RCCL) backend, world size 1 (RCCL refuses two ranks
+    on one device; the N-rank gather itself is covered by the gloo tests)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "nccl_gather_probe.py")],
+                         cwd=root, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "nccl gather ok" in out.stdout
