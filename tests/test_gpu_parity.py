@@ -479,8 +479,13 @@ def test_rccl_gather_path_world1():
     on one device; the N-rank gather itself is covered by the gloo tests)."""
     import subprocess
     import sys
+    import socket
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     out = subprocess.run([sys.executable, os.path.join(root, "tools", "nccl_gather_probe.py")],
-                         cwd=root, capture_output=True, text=True, timeout=100)
+                         cwd=root, env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "nccl gather ok" in out.stdout
