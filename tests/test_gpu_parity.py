@@ -489,3 +489,35 @@ def test_rccl_gather_path_world1():
                          cwd=root, env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "nccl gather ok" in out.stdout
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_sharded_camera_ray_lists_bitwise(oracle, world):
+    """Tile-sharded renders with the camera-ray lists in use (each rank builds the lists of its
+    own tiles, indexed by local tile): every rank's pixels equal the oracle's."""
+    from vulkancomputeraytracing_amd import scene as S
+    w, h, spp, depth = 320, 180, 2, 10
+    sc = S.builtin_scene("final")
+    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=k), sc)
+    m = vc.tile_pixel_map(w, h, world)
+    for rank in range(world):
+        pl = S.primary_lists(sc, vc.RenderDesc(width=w, height=h, rank=rank, world_size=world))
+        assert ((pl["info"] & 15) != 15).mean() > 0.5
+        kr = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h, world, rank))
+        assert kr == k  # same summation order as the 1-rank oracle render
+        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world)
+        mine = m[..., 0] == rank
+        assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], f"rank {rank}/{world}")
+
+
+def test_camera_ray_lists_switch_keeps_bits(monkeypatch):
+    """VCRT_PRIMARY_LISTS=0 (camera rays through the hierarchy) and the default give the same
+    image and segment count."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("VCRT_PRIMARY_LISTS", v)
+        outs.append(gpu_render("final", 256, 144, 4, 10))
+    assert_bitwise(outs[0][0], outs[1][0], "lists off vs on")
+    assert outs[0][1]["segments"] == outs[1][1]["segments"]
+    assert outs[0][1]["bound_tests"] > outs[1][1]["bound_tests"]  # the lists skipped box tests
