@@ -143,7 +143,8 @@ void build_primary_lists(const CullTables& ct, const float cam[12], int32_t widt
                 }
             }
         }
-        if (over) continue;
+        // ids are uint16 and offsets 28-bit: beyond that the quarter keeps no list
+        if (over || ng > 0xFFFFu || out.ids.size() + cnt >= (size_t{1} << 28)) continue;
         out.info[e] = static_cast<uint32_t>(out.ids.size()) << 4 | cnt;
         for (uint32_t k = 0; k < cnt; k++) out.ids.push_back(static_cast<uint16_t>(found[k]));
     }
