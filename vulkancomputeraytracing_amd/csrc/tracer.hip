@@ -1067,6 +1067,99 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     const uint32_t total_blocks = p.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
 
+    // Shades a traced segment (textures.glsl, or the sky of functions.glsl:85-89) and advances
+    // the lane's path: accumulate and start the next sample's camera ray (returns true), or
+    // finish the chunk (need), or continue with the bounced ray.
+    auto shade_and_advance = [&](float max_t, int best) -> bool {
+        bool ended = false, fresh_cam = false;
+        f3 contrib = mk(0.f, 0.f, 0.f);
+        if (best >= 0) {
+            const float4 cr = p.center_radius[best];
+            const float4 sh = p.shade[best];
+            const float mat = p.material[best];
+            const f3 point = add(scale(max_t, d), o);
+            const f3 normal = divs(sub(point, mk(cr.x, cr.y, cr.z)), cr.w);
+            const int type = (int)mat;
+            const f3 albedo = mk(sh.x, sh.y, sh.z);
+            const float param = sh.w;
+            // rand(dir.xy), rand(dir.xz), rand(dir.yz) for lambertian/metal (functions.glsl:43),
+            // rand(point.xy) for glass (textures.glsl:51): three sines for every hit lane
+            float s1, s2, s3;
+            sin3((type == 3) ? rand_arg(point.x, point.y) : rand_arg(d.x, d.y),
+                 rand_arg(d.x, d.z), rand_arg(d.y, d.z), s1, s2, s3);
+            const float r1 = rand_of_sin(s1);
+            if (type == 1 || type == 2) {
+                const float r2 = rand_of_sin(s2);
+                const float r3 = rand_of_sin(s3);
+                const f3 u = normalize(mk(r1, r2, r3));  // random_in_unit_sphere(dir)
+                if (type == 1) {
+                    d = add(normal, u);
+                    atten = scale(param, mul(atten, albedo));
+                } else {
+                    d = add(reflect(d, normal), scale(param, u));
+                    atten = mul(atten, albedo);
+                }
+                o = point;
+            } else if (type == 3) {
+                const f3 reflected = reflect(d, normal);
+                f3 outward;
+                float ni, cosine;
+                const float dn = dot(d, normal);
+                if (dn > 0.0f) {
+                    outward = neg(normal);
+                    ni = param;
+                    cosine = __builtin_sqrtf(1.0f - param * param * (1.0f - dn * dn));
+                } else {
+                    outward = normal;
+                    ni = 1.0f / param;
+                    cosine = -dn;
+                }
+                f3 refracted = mk(0.f, 0.f, 0.f);
+                float reflect_prob = 1.0f;
+                const float dt = dot(d, outward);
+                const float disc = 1.0f - ni * ni * (1.0f - dt * dt);
+                if (disc > 0.0f) {
+                    const float sd = __builtin_sqrtf(disc);
+                    refracted = sub(scale(ni, sub(d, scale(dt, outward))), scale(sd, outward));
+                    reflect_prob = schlick(cosine, param);
+                }
+                o = point;
+                d = (r1 < reflect_prob) ? reflected : refracted;
+            }
+            ++pass;
+            if (pass >= p.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
+        } else {
+            const float len = length(d);
+            const float t = 0.5f * (d.y / len + 1.0f);
+            const float om = 1.0f - t;
+            contrib = mul(atten, mk(om + 0.5f * t, om + 0.7f * t, om + t));
+            ended = true;
+        }
+
+        if (ended) {
+            acc = add(acc, contrib);
+            ++sample;
+            if (sample == sample_end) {
+                if ((p.flags & kFlagSlab) == 0u)
+                    p.out[out_index] =
+                        make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
+                else
+                    p.partial[(size_t)chunk * (p.local_tiles * 64u) + q] =
+                        make_float4(acc.x, acc.y, acc.z, 0.0f);
+                need = true;
+            } else {
+                const float2 jt = p.jitter[sample];
+                const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
+                o = cam;
+                d = sub(ps, cam);
+                atten = mk(1.f, 1.f, 1.f);
+                pass = 0;
+                fresh_cam = true;
+            }
+        }
+        return fresh_cam;
+    };
+
     for (;;) {
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
@@ -1182,92 +1275,63 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         // ---- shade (textures.glsl) or sky (functions.glsl:85-89) ----
         uint64_t t_shade = 0;
         if constexpr (kStats) t_shade = ticks();
-        bool ended = false;
-        f3 contrib = mk(0.f, 0.f, 0.f);
-        if (best >= 0) {
-            const float4 cr = p.center_radius[best];
-            const float4 sh = p.shade[best];
-            const float mat = p.material[best];
-            const f3 point = add(scale(max_t, d), o);
-            const f3 normal = divs(sub(point, mk(cr.x, cr.y, cr.z)), cr.w);
-            const int type = (int)mat;
-            const f3 albedo = mk(sh.x, sh.y, sh.z);
-            const float param = sh.w;
-            // rand(dir.xy), rand(dir.xz), rand(dir.yz) for lambertian/metal (functions.glsl:43),
-            // rand(point.xy) for glass (textures.glsl:51): three sines for every hit lane
-            float s1, s2, s3;
-            sin3((type == 3) ? rand_arg(point.x, point.y) : rand_arg(d.x, d.y),
-                 rand_arg(d.x, d.z), rand_arg(d.y, d.z), s1, s2, s3);
-            const float r1 = rand_of_sin(s1);
-            if (type == 1 || type == 2) {
-                const float r2 = rand_of_sin(s2);
-                const float r3 = rand_of_sin(s3);
-                const f3 u = normalize(mk(r1, r2, r3));  // random_in_unit_sphere(dir)
-                if (type == 1) {
-                    d = add(normal, u);
-                    atten = scale(param, mul(atten, albedo));
-                } else {
-                    d = add(reflect(d, normal), scale(param, u));
-                    atten = mul(atten, albedo);
-                }
-                o = point;
-            } else if (type == 3) {
-                const f3 reflected = reflect(d, normal);
-                f3 outward;
-                float ni, cosine;
-                const float dn = dot(d, normal);
-                if (dn > 0.0f) {
-                    outward = neg(normal);
-                    ni = param;
-                    cosine = __builtin_sqrtf(1.0f - param * param * (1.0f - dn * dn));
-                } else {
-                    outward = normal;
-                    ni = 1.0f / param;
-                    cosine = -dn;
-                }
-                f3 refracted = mk(0.f, 0.f, 0.f);
-                float reflect_prob = 1.0f;
-                const float dt = dot(d, outward);
-                const float disc = 1.0f - ni * ni * (1.0f - dt * dt);
-                if (disc > 0.0f) {
-                    const float sd = __builtin_sqrtf(disc);
-                    refracted = sub(scale(ni, sub(d, scale(dt, outward))), scale(sd, outward));
-                    reflect_prob = schlick(cosine, param);
-                }
-                o = point;
-                d = (r1 < reflect_prob) ? reflected : refracted;
-            }
-            ++pass;
-            if (pass >= p.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
-        } else {
-            const float len = length(d);
-            const float t = 0.5f * (d.y / len + 1.0f);
-            const float om = 1.0f - t;
-            contrib = mul(atten, mk(om + 0.5f * t, om + 0.7f * t, om + t));
-            ended = true;
-        }
-
-        if (ended) {
-            acc = add(acc, contrib);
-            ++sample;
-            if (sample == sample_end) {
-                if ((p.flags & kFlagSlab) == 0u)
-                    p.out[out_index] =
-                        make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
-                else
-                    p.partial[(size_t)chunk * (p.local_tiles * 64u) + q] =
-                        make_float4(acc.x, acc.y, acc.z, 0.0f);
-                need = true;
-            } else {
-                const float2 jt = p.jitter[sample];
-                const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
-                o = cam;
-                d = sub(ps, cam);
-                atten = mk(1.f, 1.f, 1.f);
-                pass = 0;
-            }
-        }
+        bool fresh = shade_and_advance(max_t, best);
         if constexpr (kStats) pt.shade += ticks() - t_shade;
+
+        // ---- flat scan: a camera ray started just now is traced at once from its pixel
+        //      quarter's group list (the big list, then the listed groups, per lane, with
+        //      hit_sphere's consider rule: the same sphere and t as the flat scan) and shaded,
+        //      so the lane enters the next iteration on its first bounce. The per-wave costs
+        //      of an iteration (uniform levels, ray setup, block fetch) are then shared by two
+        //      segments of such lanes. ----
+        if constexpr (kCull == 4 || kCull == 5) {
+            uint32_t inf = 15u;
+            if (fresh && p.prim_info != nullptr)
+                inf = p.prim_info[(q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)];
+            const float aa = dot(d, d);
+            const bool cam_now = (inf & 15u) != 15u && (p.flags & kFlagSceneBounded) != 0 &&
+                                 aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
+                                 fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
+            if (__ballot(cam_now)) {
+                uint32_t iters = 0;
+                float mt = 1e5f;
+                int bst = -1;
+                if (cam_now) {
+                    ++segs;
+                    CullRay r;
+                    r.ox = (v2f){o.x, o.x};
+                    r.oy = (v2f){o.y, o.y};
+                    r.oz = (v2f){o.z, o.z};
+                    const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
+                    for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres (scalar loads)
+                        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, aa, mt,
+                                            bst);
+                    const uint32_t cnt = inf & 15u;
+                    const uint16_t* ids = p.prim_ids + (inf >> 4);
+                    for (uint32_t k = 0; k < cnt; ++k) {  // the listed groups (tables in LDS
+                        ++iters;                          // or global memory)
+                        const float4* g = tgroup + 5u * ids[k];
+                        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3], idf = g[4];
+                        v2f hb01, cc01, d01, hb23, cc23, d23;
+                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+                        if (may_hit(hb01.x, cc01.x, d01.x))
+                            consider(candidate_t(hb01.x, d01.x, aa), __float_as_int(idf.x), mt, bst);
+                        if (may_hit(hb01.y, cc01.y, d01.y))
+                            consider(candidate_t(hb01.y, d01.y, aa), __float_as_int(idf.y), mt, bst);
+                        if (may_hit(hb23.x, cc23.x, d23.x))
+                            consider(candidate_t(hb23.x, d23.x, aa), __float_as_int(idf.z), mt, bst);
+                        if (may_hit(hb23.y, cc23.y, d23.y))
+                            consider(candidate_t(hb23.y, d23.y, aa), __float_as_int(idf.w), mt, bst);
+                    }
+                }
+                // issued work: the big list and the loop's passes, per wave
+                for (int off = 32; off > 0; off >>= 1)
+                    iters = max(iters, (uint32_t)__shfl_xor((int)iters, off));
+                w_groups += (uint64_t)p.nbig + iters;
+                if (cam_now) (void)shade_and_advance(mt, bst);
+            }
+        }
     }
 
     // one segment-counter atomic per wave
