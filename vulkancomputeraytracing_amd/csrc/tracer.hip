@@ -1054,6 +1054,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     const bool reverse = (p.flags & kFlagReverseOrder) != 0;
 
     bool done = false, need = true;
+    bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
     int sample = 0, sample_end = 0, pass = 0;
     uint32_t q = 0, chunk = 0, out_index = 0;
     f3 pc = mk(0.f, 0.f, 0.f), o = pc, d = pc, atten = pc, acc = pc;
@@ -1222,6 +1223,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             d = sub(ps, cam);
             atten = mk(1.f, 1.f, 1.f);
             pass = 0;
+            fresh = true;
         }
         if constexpr (kStats) pt.fetch += ticks() - t_fetch;
         const uint64_t live = __ballot(!done);
@@ -1231,6 +1233,62 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             st_active += (uint64_t)__popcll(live);
         }
         if (done) continue;
+
+        // ---- flat scan: a camera ray not yet traced (started by the last shading or by the
+        //      fetch) is traced first, from its pixel quarter's group list (the big list, then
+        //      the listed groups, per lane, with hit_sphere's consider rule: the same sphere
+        //      and t as the flat scan), and shaded; the lane then takes its first bounce
+        //      through this iteration's scan. The per-wave costs of an iteration (uniform
+        //      levels, ray setup, block fetch) are so shared by two segments of such lanes. ----
+        if constexpr (kCull == 4 || kCull == 5) {
+            uint32_t inf = 15u;
+            if (fresh && p.prim_info != nullptr)  // the list of the item's 4x4 quarter
+                inf = p.prim_info[(q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)];
+            const float aa = dot(d, d);
+            const bool cam_now = fresh && (inf & 15u) != 15u && (p.flags & kFlagSceneBounded) != 0 &&
+                                 aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
+                                 fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
+            if (__ballot(cam_now)) {
+                uint32_t iters = 0;
+                float mt = 1e5f;
+                int bst = -1;
+                if (cam_now) {
+                    ++segs;
+                    CullRay r;
+                    r.ox = (v2f){o.x, o.x};
+                    r.oy = (v2f){o.y, o.y};
+                    r.oz = (v2f){o.z, o.z};
+                    const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
+                    for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres (scalar loads)
+                        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, aa, mt,
+                                            bst);
+                    const uint32_t cnt = inf & 15u;
+                    const uint16_t* ids = p.prim_ids + (inf >> 4);
+                    for (uint32_t k = 0; k < cnt; ++k) {  // the listed groups (tables in LDS
+                        ++iters;                          // or global memory)
+                        const float4* g = tgroup + 5u * ids[k];
+                        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3], idf = g[4];
+                        v2f hb01, cc01, d01, hb23, cc23, d23;
+                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+                        if (may_hit(hb01.x, cc01.x, d01.x))
+                            consider(candidate_t(hb01.x, d01.x, aa), __float_as_int(idf.x), mt, bst);
+                        if (may_hit(hb01.y, cc01.y, d01.y))
+                            consider(candidate_t(hb01.y, d01.y, aa), __float_as_int(idf.y), mt, bst);
+                        if (may_hit(hb23.x, cc23.x, d23.x))
+                            consider(candidate_t(hb23.x, d23.x, aa), __float_as_int(idf.z), mt, bst);
+                        if (may_hit(hb23.y, cc23.y, d23.y))
+                            consider(candidate_t(hb23.y, d23.y, aa), __float_as_int(idf.w), mt, bst);
+                    }
+                }
+                // issued work: the big list and the loop's passes, per wave
+                for (int off = 32; off > 0; off >>= 1)
+                    iters = max(iters, (uint32_t)__shfl_xor((int)iters, off));
+                w_groups += (uint64_t)p.nbig + iters;
+                if (cam_now) fresh = shade_and_advance(mt, bst);
+            }
+            if (need) continue;  // that segment finished the lane's chunk
+        }
 
         // ---- one segment: scan the whole sphere list (functions.glsl:73-81) ----
         ++segs;
@@ -1275,63 +1333,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         // ---- shade (textures.glsl) or sky (functions.glsl:85-89) ----
         uint64_t t_shade = 0;
         if constexpr (kStats) t_shade = ticks();
-        bool fresh = shade_and_advance(max_t, best);
+        fresh = shade_and_advance(max_t, best);
         if constexpr (kStats) pt.shade += ticks() - t_shade;
 
-        // ---- flat scan: a camera ray started just now is traced at once from its pixel
-        //      quarter's group list (the big list, then the listed groups, per lane, with
-        //      hit_sphere's consider rule: the same sphere and t as the flat scan) and shaded,
-        //      so the lane enters the next iteration on its first bounce. The per-wave costs
-        //      of an iteration (uniform levels, ray setup, block fetch) are then shared by two
-        //      segments of such lanes. ----
-        if constexpr (kCull == 4 || kCull == 5) {
-            uint32_t inf = 15u;
-            if (fresh && p.prim_info != nullptr)
-                inf = p.prim_info[(q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)];
-            const float aa = dot(d, d);
-            const bool cam_now = (inf & 15u) != 15u && (p.flags & kFlagSceneBounded) != 0 &&
-                                 aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
-                                 fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
-            if (__ballot(cam_now)) {
-                uint32_t iters = 0;
-                float mt = 1e5f;
-                int bst = -1;
-                if (cam_now) {
-                    ++segs;
-                    CullRay r;
-                    r.ox = (v2f){o.x, o.x};
-                    r.oy = (v2f){o.y, o.y};
-                    r.oz = (v2f){o.z, o.z};
-                    const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
-                    for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres (scalar loads)
-                        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, aa, mt,
-                                            bst);
-                    const uint32_t cnt = inf & 15u;
-                    const uint16_t* ids = p.prim_ids + (inf >> 4);
-                    for (uint32_t k = 0; k < cnt; ++k) {  // the listed groups (tables in LDS
-                        ++iters;                          // or global memory)
-                        const float4* g = tgroup + 5u * ids[k];
-                        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3], idf = g[4];
-                        v2f hb01, cc01, d01, hb23, cc23, d23;
-                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
-                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
-                        if (may_hit(hb01.x, cc01.x, d01.x))
-                            consider(candidate_t(hb01.x, d01.x, aa), __float_as_int(idf.x), mt, bst);
-                        if (may_hit(hb01.y, cc01.y, d01.y))
-                            consider(candidate_t(hb01.y, d01.y, aa), __float_as_int(idf.y), mt, bst);
-                        if (may_hit(hb23.x, cc23.x, d23.x))
-                            consider(candidate_t(hb23.x, d23.x, aa), __float_as_int(idf.z), mt, bst);
-                        if (may_hit(hb23.y, cc23.y, d23.y))
-                            consider(candidate_t(hb23.y, d23.y, aa), __float_as_int(idf.w), mt, bst);
-                    }
-                }
-                // issued work: the big list and the loop's passes, per wave
-                for (int off = 32; off > 0; off >>= 1)
-                    iters = max(iters, (uint32_t)__shfl_xor((int)iters, off));
-                w_groups += (uint64_t)p.nbig + iters;
-                if (cam_now) (void)shade_and_advance(mt, bst);
-            }
-        }
     }
 
     // one segment-counter atomic per wave
