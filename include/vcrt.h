@@ -128,7 +128,8 @@ typedef struct vcrt_stats {
                            its uniform levels, node / group / candidate passes (CULL_FLAT),
                            candidate passes run, the whole wave, the big list, node pushes,
                            [17..18] shading and sky, block fetch; [19..22] flat passes:
-                           entries dealt, live lanes offered, partial passes, passes */
+                           entries dealt, live lanes offered, partial passes, passes; [23]
+                           the camera fast trace with its shading */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

@@ -715,6 +715,7 @@ struct PhaseTicks {
     uint64_t scan = 0, levels = 0, node = 0, group = 0, cand = 0, cand_passes = 0, big = 0,
              push = 0, shade = 0, fetch = 0;
     uint64_t pass_entries = 0, pass_lanes = 0, partial_passes = 0, passes = 0;
+    uint64_t cam = 0;  // the camera fast trace with its shading
 };
 
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
@@ -1241,6 +1242,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         //      through this iteration's scan. The per-wave costs of an iteration (uniform
         //      levels, ray setup, block fetch) are so shared by two segments of such lanes. ----
         if constexpr (kCull == 4 || kCull == 5) {
+            uint64_t t_cam = 0;
+            if constexpr (kStats) t_cam = ticks();
             uint32_t inf = 15u;
             if (fresh && p.prim_info != nullptr)  // the list of the item's 4x4 quarter
                 inf = p.prim_info[(q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)];
@@ -1287,6 +1290,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
                 w_groups += (uint64_t)p.nbig + iters;
                 if (cam_now) fresh = shade_and_advance(mt, bst);
             }
+            if constexpr (kStats) pt.cam += ticks() - t_cam;
             if (need) continue;  // that segment finished the lane's chunk
         }
 
@@ -1373,6 +1377,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             atomicAdd(p.debug + 20, (unsigned long long)pt.pass_lanes);
             atomicAdd(p.debug + 21, (unsigned long long)pt.partial_passes);
             atomicAdd(p.debug + 22, (unsigned long long)pt.passes);
+            atomicAdd(p.debug + 23, (unsigned long long)pt.cam);
         }
     }
 }
