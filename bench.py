@@ -187,9 +187,11 @@ def main():
     if args.validate and rank == 0:
         import numpy as np
         got = (frame if world > 1 else local.view(args.height, args.width, 4)).cpu().numpy()
+        # the reference render sums in the ranks' chunks (the default chunk follows the largest
+        # rank's share, so it is the same on every rank)
         ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
                                  max_depth=args.depth, device=device, kernel_variant=args.variant,
-                                 accumulate_chunk=args.chunk)
+                                 accumulate_chunk=st["accumulate_chunk"])
         with vc.Renderer(ref_desc, args.scene) as ref:
             ref.draw_next_frame()
             want = ref.read_framebuffer()

@@ -495,6 +495,7 @@ def test_rccl_gather_path_world1():
 def test_sharded_camera_ray_lists_bitwise(oracle, world):
     """Tile-sharded renders with the camera-ray lists in use (each rank builds the lists of its
     own tiles, indexed by local tile): every rank's pixels equal the oracle's."""
+    from vulkancomputeraytracing_amd import distributed as D
     from vulkancomputeraytracing_amd import scene as S
     w, h, spp, depth = 320, 180, 2, 10
     sc = S.builtin_scene("final")
@@ -504,9 +505,10 @@ def test_sharded_camera_ray_lists_bitwise(oracle, world):
     for rank in range(world):
         pl = S.primary_lists(sc, vc.RenderDesc(width=w, height=h, rank=rank, world_size=world))
         assert ((pl["info"] & 15) != 15).mean() > 0.5
-        kr = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h, world, rank))
+        kr = vc.renderer.effective_chunk(spp, 0, pixels=64 * D.tiles_per_rank(w, h, world))
         assert kr == k  # same summation order as the 1-rank oracle render
         part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world)
+        assert st["accumulate_chunk"] == kr
         mine = m[..., 0] == rank
         assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], f"rank {rank}/{world}")
 

@@ -401,9 +401,15 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     g.d_fb = g.d_fb_own;
     // Work decomposition: (local tile, chunk of K samples) items; chunk sums in a slab.
     g.total_pixels = g.local_tiles * 64u;  // local element slots incl. partial-tile padding
+    // The default chunk follows the largest rank's share, so every rank of a frame sums in
+    // the same order (the gathered frame equals one render with that chunk).
+    uint32_t max_tiles = 0;
+    for (int32_t rr = 0; rr < g.desc.world_size; rr++)
+        max_tiles = std::max(max_tiles, tiles_for_rank(g.desc.width, g.desc.height,
+                                                       g.desc.world_size, rr));
     g.chunk = g.desc.accumulate_chunk > 0
                   ? g.desc.accumulate_chunk
-                  : default_chunk(static_cast<uint64_t>(g.total_pixels), spp);
+                  : default_chunk(static_cast<uint64_t>(max_tiles) * 64u, spp);
     if (g.chunk > spp) g.chunk = spp;
     g.nchunks = (spp + g.chunk - 1) / g.chunk;
     {

@@ -64,7 +64,8 @@ DEFAULT_ACCUMULATE_CHUNK = 64
 def effective_chunk(spp: int, accumulate_chunk: int = 0, pixels: int | None = None) -> int:
     """Samples per work item the renderer uses (the oracle's `chunk` for the same order).
     Mirrors default_chunk() in csrc/capi.cpp when accumulate_chunk is 0; `pixels` is the
-    rank's tile slots (64 per 8x8 tile, see tile_slots)."""
+    largest rank's tile slots (64 per 8x8 tile: tile_slots(w, h) for one rank,
+    64 * distributed.tiles_per_rank(w, h, world) for a sharded frame)."""
     if accumulate_chunk > 0:
         k = accumulate_chunk
     else:
