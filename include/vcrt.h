@@ -93,10 +93,14 @@ typedef struct vcrt_render_desc {
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
     int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 4 while the
-                                 rank has < 2^24 work items). A pixel's samples are summed
-                                 in order within a chunk and the chunk sums in chunk order;
-                                 >= samples_per_pixel reproduces the reference's sequential
-                                 sum (shader.comp:46-54) exactly. */
+                                 whole frame has < 2^24 items, at least spp / 512; a function
+                                 of width, height and spp only: vcrt_work_chunk). A pixel's
+                                 samples are summed in fp32 in order within a chunk; one chunk
+                                 (>= samples_per_pixel) is divided in fp32, the reference's
+                                 sequential sum (shader.comp:46-56) exactly; several chunk sums
+                                 are quantized to 2^-32 and added exactly, so the image does not
+                                 depend on the schedule or the world size. At most 512 chunks
+                                 per pixel (progressive frames included). */
     int32_t progressive; /* 0: every DrawNextFrame re-renders samples 0..spp-1 (the reference,
                             Linux.cpp:362-366). 1: frame f renders samples f*spp..(f+1)*spp-1 and
                             the framebuffer holds the average of all frames so far (the same
@@ -111,7 +115,7 @@ typedef struct vcrt_stats {
     uint64_t samples;      /* local_rows * width * spp */
     double kernel_ms;      /* tracer kernel time, HIP events on the render stream */
     double frame_ms;       /* host wall time of the last vcrt_draw_next_frame */
-    double resolve_ms;     /* chunk-sum resolve kernel time (0 when one chunk) */
+    double resolve_ms;     /* resolve kernel time (exact chunk sums -> pixels; 0: one chunk) */
     int32_t frames;        /* frames drawn since vcrt_begin */
     int32_t grid_blocks, block_threads, kernel_variant;
     int32_t local_tiles;   /* 8x8 tiles this rank renders */
@@ -137,6 +141,9 @@ typedef struct vcrt_stats {
 vcrt_result vcrt_default_desc(vcrt_render_desc* desc);
 
 vcrt_result vcrt_begin(const vcrt_render_desc* desc);
+/* Samples per work item (the accumulation chunk) that vcrt_begin(desc) uses; host only, no
+ * GPU. Negative VkResult for an invalid desc. */
+int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
  * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final
  * scene at 1080p, ~0.4 s for 4100 spheres at 4K). vcrt_begin sets the final scene. */

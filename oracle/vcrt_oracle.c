@@ -302,7 +302,7 @@ void oracle_ray_color(const oracle_sphere* world, int32_t n, const float origin[
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* per-pixel driver: shader.comp:42-57, multithreaded over rows                          */
+/* per-pixel driver: shader.comp:42-57, multithreaded over rows or pixels                  */
 
 typedef struct {
     const oracle_config* cfg;
@@ -312,57 +312,88 @@ typedef struct {
     const float* jitter; /* 2*spp: (-0.5+rand(i,i), -0.5+rand(i+1,i+1)) */
     float cam[15];
     int32_t row_begin, row_end, row_step, nrows;
-    volatile int next; /* row counter */
+    const int32_t* pixels; /* pixel-list mode: (x, y) pairs, one output rgba per pair */
+    int32_t npixels;
+    volatile int next; /* row (or pixel-batch) counter */
     pthread_mutex_t lock;
     uint64_t segments;
 } render_job;
 
-static void render_row(render_job* job, int y, uint64_t* segs) {
+/* One pixel (shader.comp:43-57) into px[4]. Accumulation (vulkancomputeraytracing_amd/csrc/
+ * vcrt_math.h "Accumulation"): the samples are cut into chunks of K (restarting at every
+ * progressive frame of frame_spp samples); a chunk is summed in fp32 in sample order, as the
+ * reference sums (shader.comp:46-54). A single chunk (K >= spp, no progressive frames) is then
+ * divided by SAMPLES_PER_PIXEL in fp32: the reference's own arithmetic (shader.comp:56).
+ * Otherwise every chunk sum S is quantized to q = RN_even(S * 2^32) (|S| < 2^12; a NaN, infinite
+ * or larger sum makes the pixel NaN), the q are added exactly (integers below 2^53 in double),
+ * and the pixel is (float)((sum * 2^-32) / spp). */
+static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* segs) {
     const oracle_config* cfg = job->cfg;
     v3 p00 = V(job->cam[0], job->cam[1], job->cam[2]);
     v3 du = V(job->cam[3], job->cam[4], job->cam[5]);
     v3 dv = V(job->cam[6], job->cam[7], job->cam[8]);
     v3 center = V(job->cam[9], job->cam[10], job->cam[11]);
-    for (int x = 0; x < cfg->width; x++) {
-        v3 pc = vadd(vadd(p00, vscale((float)x, du)), vscale((float)y, dv));
-        const int block = (cfg->frame_spp <= 0 || cfg->frame_spp > cfg->spp) ? cfg->spp
-                                                                            : cfg->frame_spp;
-        const int chunk =
-            (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block) ? block
-                                                                            : cfg->accumulate_chunk;
-        v3 acc = V(0.0f, 0.0f, 0.0f);
-        for (int c0 = 0; c0 < cfg->spp;) {
-            v3 part = V(0.0f, 0.0f, 0.0f);
-            const int block_end = (c0 / block + 1) * block;
-            int c1 = c0 + chunk < block_end ? c0 + chunk : block_end;
-            if (c1 > cfg->spp) c1 = cfg->spp;
-            for (int i = c0; i < c1; i++) {
-                float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
-                v3 rs = vadd(vscale(jx, du), vscale(jy, dv));
-                v3 ps = vadd(pc, rs);
-                v3 dir = vsub(ps, center);
-                part = vadd(part, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
-            }
-            acc = vadd(acc, part); /* one chunk: 0 + part == part, the sequential sum */
-            c0 = c1;
+    v3 pc = vadd(vadd(p00, vscale((float)x, du)), vscale((float)y, dv));
+    const int block = (cfg->frame_spp <= 0 || cfg->frame_spp > cfg->spp) ? cfg->spp
+                                                                        : cfg->frame_spp;
+    const int chunk =
+        (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block) ? block
+                                                                        : cfg->accumulate_chunk;
+    const int single = cfg->frame_spp <= 0 && chunk >= cfg->spp;
+    double sum[3] = {0.0, 0.0, 0.0};
+    v3 part = V(0.0f, 0.0f, 0.0f);
+    for (int c0 = 0; c0 < cfg->spp;) {
+        part = V(0.0f, 0.0f, 0.0f);
+        const int block_end = (c0 / block + 1) * block;
+        int c1 = c0 + chunk < block_end ? c0 + chunk : block_end;
+        if (c1 > cfg->spp) c1 = cfg->spp;
+        for (int i = c0; i < c1; i++) {
+            float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
+            v3 rs = vadd(vscale(jx, du), vscale(jy, dv));
+            v3 ps = vadd(pc, rs);
+            v3 dir = vsub(ps, center);
+            part = vadd(part, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
         }
-        float* px = job->rgba + ((size_t)y * cfg->width + x) * 4;
-        px[0] = acc.x / (float)cfg->spp;
-        px[1] = acc.y / (float)cfg->spp;
-        px[2] = acc.z / (float)cfg->spp;
-        px[3] = 1.0f;
+        const float m = fmaxf(fmaxf(fabsf(part.x), fabsf(part.y)), fabsf(part.z));
+        if (isnan(part.x) || isnan(part.y) || isnan(part.z) || !(m < 4096.0f)) {
+            sum[0] = sum[1] = sum[2] = NAN;
+        } else {
+            sum[0] += (double)rintf(part.x * 0x1p32f);
+            sum[1] += (double)rintf(part.y * 0x1p32f);
+            sum[2] += (double)rintf(part.z * 0x1p32f);
+        }
+        c0 = c1;
     }
+    if (single) { /* color /= SAMPLES_PER_PIXEL in fp32 (shader.comp:56) */
+        px[0] = part.x / (float)cfg->spp;
+        px[1] = part.y / (float)cfg->spp;
+        px[2] = part.z / (float)cfg->spp;
+    } else {
+        for (int k = 0; k < 3; k++) px[k] = (float)((sum[k] * 0x1p-32) / (double)cfg->spp);
+    }
+    px[3] = 1.0f;
 }
 
 static void* render_worker(void* arg) {
     render_job* job = (render_job*)arg;
+    const oracle_config* cfg = job->cfg;
     uint64_t segs = 0;
+    const int batch = 16; /* pixel-list mode hands out pixels 16 at a time */
+    const int units = job->pixels ? (job->npixels + batch - 1) / batch : job->nrows;
     for (;;) {
         pthread_mutex_lock(&job->lock);
         int k = job->next++;
         pthread_mutex_unlock(&job->lock);
-        if (k >= job->nrows) break;
-        render_row(job, job->row_begin + k * job->row_step, &segs);
+        if (k >= units) break;
+        if (job->pixels) {
+            for (int p = k * batch; p < job->npixels && p < (k + 1) * batch; p++)
+                render_pixel(job, job->pixels[2 * p], job->pixels[2 * p + 1], job->rgba + 4 * p,
+                             &segs);
+        } else {
+            int y = job->row_begin + k * job->row_step;
+            for (int x = 0; x < cfg->width; x++)
+                render_pixel(job, x, y, job->rgba + ((size_t)y * cfg->width + x) * 4, &segs);
+        }
     }
     pthread_mutex_lock(&job->lock);
     job->segments += segs;
@@ -370,11 +401,42 @@ static void* render_worker(void* arg) {
     return NULL;
 }
 
+static int run_job(render_job* job, int32_t threads, uint64_t* segments) {
+    const oracle_config* cfg = job->cfg;
+    oracle_camera(cfg, job->cam);
+    float* jit = (float*)malloc(sizeof(float) * 2 * (size_t)cfg->spp);
+    if (!jit) return -1;
+    for (int i = 0; i < cfg->spp; i++) {
+        jit[2 * i] = -0.5f + oracle_rand((float)i, (float)i);
+        jit[2 * i + 1] = -0.5f + oracle_rand((float)(i + 1), (float)(i + 1));
+    }
+    job->jitter = jit;
+    pthread_mutex_init(&job->lock, NULL);
+    if (threads <= 1) {
+        render_worker(job);
+    } else {
+        pthread_t* tids = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+        int started = 0;
+        for (int t = 0; tids && t < threads; t++)
+            if (pthread_create(&tids[t], NULL, render_worker, job) == 0) started++;
+        if (started == 0) render_worker(job);
+        for (int t = 0; t < started; t++) pthread_join(tids[t], NULL);
+        free(tids);
+    }
+    pthread_mutex_destroy(&job->lock);
+    free(jit);
+    if (segments) *segments = job->segments;
+    return 0;
+}
+
+static int config_ok(const oracle_config* cfg) {
+    return cfg && cfg->width > 0 && cfg->height > 0 && cfg->spp > 0 && cfg->max_depth >= 0;
+}
+
 int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t n, float* rgba,
                   int32_t row_begin, int32_t row_end, int32_t row_step, int32_t threads,
                   uint64_t* segments) {
-    if (!cfg || !rgba || n < 0 || (n > 0 && !world)) return -1;
-    if (cfg->width <= 0 || cfg->height <= 0 || cfg->spp <= 0 || cfg->max_depth < 0) return -1;
+    if (!config_ok(cfg) || !rgba || n < 0 || (n > 0 && !world)) return -1;
     if (row_step <= 0) row_step = 1;
     if (row_begin < 0) row_begin = 0;
     if (row_end > cfg->height) row_end = cfg->height;
@@ -388,30 +450,28 @@ int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t 
     job.row_end = row_end;
     job.row_step = row_step;
     job.nrows = row_end > row_begin ? (row_end - row_begin + row_step - 1) / row_step : 0;
-    oracle_camera(cfg, job.cam);
-    float* jit = (float*)malloc(sizeof(float) * 2 * (size_t)cfg->spp);
-    if (!jit) return -1;
-    for (int i = 0; i < cfg->spp; i++) {
-        jit[2 * i] = -0.5f + oracle_rand((float)i, (float)i);
-        jit[2 * i + 1] = -0.5f + oracle_rand((float)(i + 1), (float)(i + 1));
-    }
-    job.jitter = jit;
-    pthread_mutex_init(&job.lock, NULL);
-    if (threads <= 1) {
-        render_worker(&job);
-    } else {
-        pthread_t* tids = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
-        int started = 0;
-        for (int t = 0; t < threads; t++)
-            if (pthread_create(&tids[t], NULL, render_worker, &job) == 0) started++;
-        if (started == 0) render_worker(&job);
-        for (int t = 0; t < started; t++) pthread_join(tids[t], NULL);
-        free(tids);
-    }
-    pthread_mutex_destroy(&job.lock);
-    free(jit);
-    if (segments) *segments = job.segments;
-    return 0;
+    return run_job(&job, threads, segments);
+}
+
+int oracle_render_pixels(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
+                         const int32_t* xy, int32_t npixels, float* rgba, int32_t threads,
+                         uint64_t* segments) {
+    if (!config_ok(cfg) || npixels < 0 || (npixels > 0 && (!xy || !rgba)) || n < 0 ||
+        (n > 0 && !world))
+        return -1;
+    for (int32_t p = 0; p < npixels; p++)
+        if (xy[2 * p] < 0 || xy[2 * p] >= cfg->width || xy[2 * p + 1] < 0 ||
+            xy[2 * p + 1] >= cfg->height)
+            return -1;
+    render_job job;
+    memset(&job, 0, sizeof(job));
+    job.cfg = cfg;
+    job.world = world;
+    job.n = n;
+    job.rgba = rgba;
+    job.pixels = xy;
+    job.npixels = npixels;
+    return run_job(&job, threads, segments);
 }
 
 /* ------------------------------------------------------------------------------------ */

@@ -34,12 +34,13 @@ typedef struct oracle_config {
     int32_t width, height, spp, max_depth;
     float lookfrom[3], lookat[3], vup[3];
     float vfov;
-    /* Accumulation order. 0 or >= spp: the reference's sequential sum (shader.comp:46-54).
-     * K < spp: samples summed sequentially within chunks of K, chunk sums then added in chunk
-     * order (the order the GPU uses when it splits a pixel's samples into work items). */
+    /* Accumulation (see oracle_render_pixel in vcrt_oracle.c and DESIGN.md section 3). The
+     * samples are cut into chunks of accumulate_chunk (0 or >= spp: one chunk), restarting at
+     * every progressive frame of frame_spp samples (0: one frame). Each chunk is summed in fp32
+     * in sample order. One chunk and no frames: sum / spp in fp32, the reference's sequential
+     * sum (shader.comp:46-56) exactly. Otherwise the chunk sums are quantized to 2^-32 and
+     * added exactly, then divided in double: the GPU's order-independent combination. */
     int32_t accumulate_chunk;
-    /* Chunk boundaries also restart every frame_spp samples (progressive frames of frame_spp
-     * samples each); 0 = one frame of spp samples. */
     int32_t frame_spp;
 } oracle_config;
 
@@ -57,6 +58,12 @@ void oracle_camera(const oracle_config* cfg, float out[15]);
 int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
                   float* rgba, int32_t row_begin, int32_t row_end, int32_t row_step,
                   int32_t threads, uint64_t* segments);
+
+/* The same for a list of pixels: xy = npixels (x, y) pairs, rgba = 4 floats per pixel in list
+ * order. Returns 0 on success, -1 on a bad argument (pixel outside the frame). */
+int oracle_render_pixels(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
+                         const int32_t* xy, int32_t npixels, float* rgba, int32_t threads,
+                         uint64_t* segments);
 
 /* Per-pixel radiance of one sample (ray_color), for KATs. */
 void oracle_ray_color(const oracle_sphere* world, int32_t n, const float origin[3],

@@ -55,6 +55,11 @@ class Oracle:
                                     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                     ctypes.c_int32, ctypes.c_int32,
                                     ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_render_pixels.restype = ctypes.c_int
+        L.oracle_render_pixels.argtypes = [ctypes.POINTER(OracleConfig), ctypes.c_void_p,
+                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_int32,
+                                           ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_ray_color.restype = None
         L.oracle_ray_color.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
@@ -109,6 +114,21 @@ class Oracle:
         if r != 0:
             raise ValueError("oracle_render rejected its arguments")
         return img, segs.value
+
+    def render_pixels(self, cfg: OracleConfig, spheres: np.ndarray, xy, threads: int = 0):
+        """Pixels xy [(x, y), ...] of a W x H frame -> (float32 [len(xy), 4], segments)."""
+        spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+        xy = np.ascontiguousarray(np.asarray(xy, dtype=np.int32).reshape(-1, 2))
+        out = np.zeros((len(xy), 4), dtype=np.float32)
+        if threads <= 0:
+            threads = min(os.cpu_count() or 1, 16)
+        segs = ctypes.c_uint64()
+        r = self.lib.oracle_render_pixels(ctypes.byref(cfg), spheres.ctypes.data, len(spheres),
+                                          xy.ctypes.data, len(xy), out.ctypes.data, threads,
+                                          ctypes.byref(segs))
+        if r != 0:
+            raise ValueError("oracle_render_pixels rejected its arguments")
+        return out, segs.value
 
     def encode_srgb8(self, rgba: np.ndarray) -> np.ndarray:
         rgba = np.ascontiguousarray(rgba, dtype=np.float32)

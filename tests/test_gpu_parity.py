@@ -30,6 +30,12 @@ def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0,
         return r.read_framebuffer(), r.stats()
 
 
+def chunk_of(w, h, spp, chunk=0):
+    """The accumulation chunk the renderer uses (C ABI vcrt_work_chunk, no re-implementation)."""
+    return vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
+                                                accumulate_chunk=chunk))
+
+
 def bits(a):
     return np.ascontiguousarray(a).view(np.uint32)
 
@@ -69,8 +75,7 @@ def expected_variant(variant, nspheres):
 def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     got, st = gpu_render(scene, w, h, spp, depth, variant)
     # default work split: the oracle sums in the same order (chunks of accumulate_chunk)
-    assert st["accumulate_chunk"] == vc.renderer.effective_chunk(spp, 0,
-                                                                 pixels=vc.tile_slots(w, h))
+    assert st["accumulate_chunk"] == chunk_of(w, h, spp)
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth,
                                                   chunk=st["accumulate_chunk"]),
                                     oracle.scene(scene))
@@ -88,7 +93,7 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     ("final", 40, 24, 33, 10, 33),   # one chunk = the reference's sequential order
 ])
 def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, variant):
-    k = vc.renderer.effective_chunk(spp, chunk, pixels=vc.tile_slots(w, h))
+    k = chunk_of(w, h, spp, chunk)
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
     got, st = gpu_render(scene, w, h, spp, depth, variant, chunk=chunk)
     assert st["accumulate_chunk"] == k
@@ -105,7 +110,8 @@ def test_golden_oracle_images():
     from tests.golden.make_golden import IMAGES
     data = np.load(os.path.join(GOLDEN, "oracle_images.npz"))
     for name, scene, w, h, spp, depth in IMAGES:
-        got, st = gpu_render(scene, w, h, spp, depth)
+        # the goldens hold the reference's sequential sum: one chunk per pixel
+        got, st = gpu_render(scene, w, h, spp, depth, chunk=spp)
         assert_bitwise(got, data[name], name)
         assert st["segments"] == int(data[name + "__segments"][0])
 
@@ -127,7 +133,7 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
     # (VCRT_CULL_LANE_TABLES forces either; the default picks LDS up to 32 KB)
     monkeypatch.setenv("VCRT_CULL_LANE_TABLES", tables)
     w, h, spp, depth = 40, 24, 3, 12
-    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    k = chunk_of(w, h, spp, 0)
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
     got, st = gpu_render(scene, w, h, spp, depth, vc.KERNEL_CULL_LANE)
     assert st["kernel_variant"] == vc.KERNEL_CULL_LANE
@@ -192,7 +198,7 @@ def test_large_random_scene_all_variants(oracle, n):
     sc = random_large_scene(n, seed=n)
     w, h, spp, depth = 40, 24, 2, 8
     cfg = dict(lookfrom=(-80, 10, 5), lookat=(0, 0, 0), vfov=50)
-    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    k = chunk_of(w, h, spp, 0)
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
     for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
@@ -212,7 +218,7 @@ def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
     sc = culling_torture_scene()
     assert len(sc) >= 16
     cfg = dict(lookfrom=(6, 2.5, 5), lookat=(0, 0.6, 0), vfov=45)
-    k = vc.renderer.effective_chunk(spp, chunk, pixels=vc.tile_slots(w, h))
+    k = chunk_of(w, h, spp, chunk)
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
     for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
@@ -240,7 +246,7 @@ def test_camera_ray_lists_bitwise(oracle, cam):
     sc = S.builtin_scene("final")
     pl = S.primary_lists(sc, vc.RenderDesc(width=w, height=h, **cam))
     assert ((pl["info"] & 15) != 15).mean() > 0.3  # the lists are in use
-    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    k = chunk_of(w, h, spp, 0)
     want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cam), sc)
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
                          **cam)
@@ -499,16 +505,15 @@ def test_sharded_camera_ray_lists_bitwise(oracle, world):
     from vulkancomputeraytracing_amd import scene as S
     w, h, spp, depth = 320, 180, 2, 10
     sc = S.builtin_scene("final")
-    k = vc.renderer.effective_chunk(spp, 0, pixels=vc.tile_slots(w, h))
+    k = chunk_of(w, h, spp, 0)
     want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=k), sc)
     m = vc.tile_pixel_map(w, h, world)
     for rank in range(world):
         pl = S.primary_lists(sc, vc.RenderDesc(width=w, height=h, rank=rank, world_size=world))
         assert ((pl["info"] & 15) != 15).mean() > 0.5
-        kr = vc.renderer.effective_chunk(spp, 0, pixels=64 * D.tiles_per_rank(w, h, world))
-        assert kr == k  # same summation order as the 1-rank oracle render
         part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world)
-        assert st["accumulate_chunk"] == kr
+        # the default chunk is a function of the frame, not of the rank: the 1-rank order
+        assert st["accumulate_chunk"] == k
         mine = m[..., 0] == rank
         assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], f"rank {rank}/{world}")
 

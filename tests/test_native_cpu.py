@@ -151,3 +151,31 @@ def test_srgb8_thresholds_agree_with_oracle(oracle):
     enc = oracle.encode_srgb8(px)
     assert np.array_equal(enc[:, 0], np.arange(1, 256, dtype=np.uint8))
     assert np.array_equal(enc[:, 1], np.arange(0, 255, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (37, 23),
+                                 (1, 1)])
+@pytest.mark.parametrize("spp", [1, 3, 16, 64, 256, 1024, 4096, 100000])
+def test_work_chunk_is_a_function_of_the_frame(w, h, spp):
+    """vcrt_work_chunk (the accumulation chunk vcrt_begin uses; host only): the same for every
+    rank and world size of a frame (a sharded frame sums like a 1-GPU render), at most spp, at
+    most 512 chunks per pixel, and an explicit accumulate_chunk is taken as given."""
+    k = vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp))
+    assert 1 <= k <= spp
+    assert -(-spp // k) <= 512
+    assert k == spp or k >= 4
+    for world in (2, 3, 8):
+        for rank in (0, world - 1):
+            kr = vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
+                                                      rank=rank, world_size=world))
+            assert kr == k
+    assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
+                                                accumulate_chunk=7)) == min(7, spp)
+    if (w, h, spp) == (1920, 1080, 1024):
+        assert k == 64  # the bench config: 16 chunks of 64 samples
+
+
+def test_work_chunk_rejects_invalid_desc():
+    lib = N.lib()
+    d = vc.RenderDesc(width=0, height=10, samples_per_pixel=4).to_c()
+    assert lib.vcrt_work_chunk(ctypes.byref(d)) == N.VK_ERROR_INITIALIZATION_FAILED

@@ -160,6 +160,59 @@ def test_chunked_order_is_close_to_sequential(oracle):
     assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
 
 
+def _chunked_pixel(oracle, cfg, scene, x, y, k):
+    """DESIGN.md 3 / vcrt_math.h "Accumulation" restated in numpy from per-sample radiance:
+    fp32 chunk sums in sample order, each quantized to RN_even(S * 2^32), summed as integers,
+    one double division, rounded to fp32."""
+    cam = oracle.camera(cfg)
+    p00, du, dv, center = cam[0:3], cam[3:6], cam[6:9], cam[9:12]
+    f = np.float32
+    pc = (p00 + f(x) * du) + f(y) * dv
+    total = [0, 0, 0]
+    for c0 in range(0, cfg.spp, k):
+        part = np.zeros(3, dtype=np.float32)
+        for i in range(c0, min(c0 + k, cfg.spp)):
+            jx = f(-0.5) + f(oracle.rand(float(i), float(i)))
+            jy = f(-0.5) + f(oracle.rand(float(i + 1), float(i + 1)))
+            ps = pc + (jx * du + jy * dv)
+            c, _ = oracle.ray_color(scene, center, ps - center, cfg.max_depth)
+            part = part + c
+        assert np.abs(part).max() < 4096
+        for ch in range(3):
+            total[ch] += int(np.rint(part[ch] * f(2.0 ** 32)))
+    return np.array([(t * 2.0 ** -32) / cfg.spp for t in total], dtype=np.float64).astype(
+        np.float32)
+
+
+def test_chunk_combination_definition(oracle):
+    """The oracle's chunked accumulation equals its definition, recomputed from per-sample
+    radiance with integer arithmetic."""
+    scene = oracle.scene("final")
+    cfg = oracle.config(20, 12, 24, 10, chunk=5)
+    img, _ = oracle.render(cfg, scene)
+    for x, y in [(0, 0), (7, 5), (19, 11), (13, 8), (3, 10)]:
+        want = _chunked_pixel(oracle, cfg, scene, x, y, 5)
+        assert np.array_equal(img[y, x, :3].view(np.uint32), want.view(np.uint32)), (x, y)
+        assert img[y, x, 3] == 1.0
+
+
+def test_render_pixels_equals_rows(oracle):
+    scene = oracle.scene("three")
+    for chunk in (0, 4):
+        cfg = oracle.config(40, 24, 6, 8, chunk=chunk)
+        full, segs = oracle.render(cfg, scene)
+        xy = [(x, y) for y in range(24) for x in range(40)]
+        px, psegs = oracle.render_pixels(cfg, scene, xy)
+        assert psegs == segs
+        assert np.array_equal(px.view(np.uint32), full.reshape(-1, 4).view(np.uint32))
+        sub = [(39, 23), (0, 0), (17, 9)]
+        px2, _ = oracle.render_pixels(cfg, scene, sub)
+        for k, (x, y) in enumerate(sub):
+            assert np.array_equal(px2[k].view(np.uint32), full[y, x].view(np.uint32))
+    with pytest.raises(ValueError):
+        oracle.render_pixels(cfg, scene, [(40, 0)])
+
+
 def _srgb_reference(c):
     c = np.nan_to_num(np.asarray(c, dtype=np.float64), nan=0.0)
     c = np.clip(c, 0.0, 1.0)
@@ -185,7 +238,7 @@ def test_progressive_frame_blocks(oracle):
     a, sa = oracle.render(oracle.config(24, 16, 8, 6, chunk=4, frame_spp=4), scene)
     b, sb = oracle.render(oracle.config(24, 16, 8, 6, chunk=4), scene)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and sa == sb
-    # frame blocks restart chunks: (3,1),(3,1) differs from (3,3,2) only in summation order
+    # frame blocks restart chunks: (3,1),(3,1) differs from (3,3,2) only in the chunk sums
     c, _ = oracle.render(oracle.config(24, 16, 8, 6, chunk=3, frame_spp=4), scene)
     d, _ = oracle.render(oracle.config(24, 16, 8, 6, chunk=3), scene)
     assert np.abs(c.astype(np.float64) - d).max() < 1e-6

@@ -107,6 +107,7 @@ class vcrt_stats(ctypes.Structure):
 SIGNATURES = {
     "vcrt_default_desc": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_begin": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
+    "vcrt_work_chunk": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_set_scene": (ctypes.c_int32, [ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_draw_next_frame": (ctypes.c_int32, []),
     "vcrt_end": (ctypes.c_int32, []),
@@ -186,6 +187,13 @@ class VcrtError(RuntimeError):
     def __init__(self, where: str, code: int):
         super().__init__(f"{where} failed: {result_string(code)} ({code})")
         self.code = code
+
+
+def check_count(where: str, value: int) -> int:
+    """A count-or-VkResult return: negative values are errors."""
+    if value < 0:
+        raise VcrtError(where, value)
+    return value
 
 
 def check(where: str, code: int) -> int:

@@ -79,9 +79,9 @@ struct RendererState {
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
     uint32_t total_pixels = 0, total_items = 0;
-    float4* d_partial = nullptr;  // [nchunks][total_pixels] chunk sums
-    float4* d_accum = nullptr;    // progressive running sums [total_pixels]
-    uint64_t accumulated = 0;     // samples per pixel accumulated (progressive)
+    bool direct = false;  // one item per pixel, not progressive: lanes write pixels (kFlagDirect)
+    double* d_accum = nullptr;  // [total_pixels][4] exact sums of the quantized chunk sums
+    uint64_t accumulated = 0;               // samples per pixel accumulated (progressive)
     std::vector<float2> jitter_host;
     float* d_srgb_thresholds = nullptr;
     uchar4* d_srgb = nullptr;
@@ -107,14 +107,26 @@ RendererState g;
     } while (0)
 
 // Samples per work item when the caller leaves it to us: 64, halved (down to 4) while the
-// rank's work would be fewer than 2^24 items, so every lane of the persistent grid (~400k
-// lanes on MI355X) still gets ~40 items and the drain at the end stays short. A function of
-// the configuration only, so the summation order does not depend on the device.
-int32_t default_chunk(uint64_t pixels, int32_t spp) {
+// frame would be fewer than 2^24 items, so every lane of the persistent grid (~400k lanes on
+// MI355X) still gets ~40 items and the drain at the end stays short; at least spp / 512, so
+// a pixel has at most kAccumMaxChunks chunks. A function of the frame only (its 8x8-tile
+// slots and spp), not of the rank or the world size, so a sharded frame is bit-identical to a
+// one-GPU render (vcrt_math.h "Accumulation").
+int32_t default_chunk(uint64_t frame_slots, int32_t spp) {
     int32_t k = kDefaultChunk;
-    while (k > 4 && pixels * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 24))
+    while (k > 4 && frame_slots * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 24))
         k /= 2;
-    return k;
+    const int32_t k_min = (spp + vcrt::kAccumMaxChunks - 1) / vcrt::kAccumMaxChunks;
+    return std::max(k, k_min);
+}
+
+// Samples per work item for a desc: its accumulate_chunk (capped at spp), else the default.
+int32_t work_chunk(const vcrt_render_desc& d) {
+    const uint64_t frame_slots = 64ull * static_cast<uint64_t>((d.width + 7) / 8) *
+                                 static_cast<uint64_t>((d.height + 7) / 8);
+    const int32_t k = d.accumulate_chunk > 0 ? d.accumulate_chunk
+                                             : default_chunk(frame_slots, d.samples_per_pixel);
+    return std::min(k, d.samples_per_pixel);
 }
 
 // Jitter of sample indices base .. base+n-1 (shader.comp:48 depends only on the index).
@@ -280,6 +292,7 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (d.width <= 0 || d.height <= 0 || d.samples_per_pixel <= 0 || d.max_depth < 0)
         return false;
     if (static_cast<int64_t>(d.width) * d.height > (int64_t{1} << 31)) return false;
+    if (d.width > 65535 || d.height > 65535) return false;  // kernels pack y << 16 | x
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
     if (d.progressive != 0 && d.progressive != 1) return false;
@@ -316,6 +329,11 @@ vcrt_result vcrt_default_desc(vcrt_render_desc* d) {
     d->world_size = 1;
     d->kernel_variant = VCRT_KERNEL_AUTO;
     return VCRT_SUCCESS;
+}
+
+int32_t vcrt_work_chunk(const vcrt_render_desc* desc) {
+    if (!desc || !desc_valid(*desc)) return VCRT_ERROR_INITIALIZATION_FAILED;
+    return work_chunk(*desc);
 }
 
 vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
@@ -399,33 +417,23 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         if ((r = to_vk(hipMemset(g.d_fb_own, 0, g.fb_bytes))) != VK_SUCCESS) return fail(r);
     }
     g.d_fb = g.d_fb_own;
-    // Work decomposition: (local tile, chunk of K samples) items; chunk sums in a slab.
+    // Work decomposition: (local tile, chunk of K samples) items; a pixel's chunk sums are
+    // combined exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks of them.
     g.total_pixels = g.local_tiles * 64u;  // local element slots incl. partial-tile padding
-    // The default chunk follows the largest rank's share, so every rank of a frame sums in
-    // the same order (the gathered frame equals one render with that chunk).
-    uint32_t max_tiles = 0;
-    for (int32_t rr = 0; rr < g.desc.world_size; rr++)
-        max_tiles = std::max(max_tiles, tiles_for_rank(g.desc.width, g.desc.height,
-                                                       g.desc.world_size, rr));
-    g.chunk = g.desc.accumulate_chunk > 0
-                  ? g.desc.accumulate_chunk
-                  : default_chunk(static_cast<uint64_t>(max_tiles) * 64u, spp);
-    if (g.chunk > spp) g.chunk = spp;
+    g.chunk = work_chunk(g.desc);
     g.nchunks = (spp + g.chunk - 1) / g.chunk;
+    if (g.nchunks > vcrt::kAccumMaxChunks) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
+    g.direct = g.nchunks == 1 && !g.desc.progressive;
     {
         const uint64_t items =
             static_cast<uint64_t>(g.total_pixels) * static_cast<uint64_t>(g.nchunks);
         if (items >= (uint64_t{1} << 31)) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
         g.total_items = static_cast<uint32_t>(items);
     }
-    if (g.desc.progressive && g.total_pixels) {
-        const size_t bytes = sizeof(float4) * g.total_pixels;
+    if (!g.direct && g.total_pixels) {  // 32 B per pixel, whatever the spp
+        const size_t bytes = 32u * static_cast<size_t>(g.total_pixels);
         if ((r = to_vk(hipMalloc(&g.d_accum, bytes))) != VK_SUCCESS) return fail(r);
         if ((r = to_vk(hipMemset(g.d_accum, 0, bytes))) != VK_SUCCESS) return fail(r);
-    }
-    if ((g.nchunks > 1 || g.desc.progressive) && g.total_pixels) {
-        const size_t slab = sizeof(float4) * g.total_pixels * static_cast<size_t>(g.nchunks);
-        if ((r = to_vk(hipMalloc(&g.d_partial, slab))) != VK_SUCCESS) return fail(r);
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
     if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e) != 0;
@@ -545,7 +553,7 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     g.nspheres = count;
     g.stats.nspheres = count;
     g.accumulated = 0;  // a new scene restarts progressive accumulation
-    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, sizeof(float4) * g.total_pixels));
+    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
     g.scene_bounded = true;
     for (int32_t i = 0; i < count; i++) {
         const vcrt_sphere& sp = spheres[i];
@@ -570,7 +578,14 @@ vcrt_result vcrt_draw_next_frame(void) {
         VkResult r = launch(g.k_fill, grid, 256, 0, fp);
         if (r != VK_SUCCESS) return r;
     }
-    const bool slab = g.nchunks > 1 || g.desc.progressive;
+    const uint64_t spp_total =
+        (g.desc.progressive ? g.accumulated : 0) + static_cast<uint64_t>(g.desc.samples_per_pixel);
+    // progressive frames add chunks to the pixels' exact sums: at most kAccumMaxChunks in all
+    if (g.desc.progressive &&
+        (g.accumulated / static_cast<uint64_t>(g.desc.samples_per_pixel) + 1) *
+                static_cast<uint64_t>(g.nchunks) >
+            static_cast<uint64_t>(vcrt::kAccumMaxChunks))
+        return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
     if (g.desc.progressive && g.accumulated > 0) {
         // progressive frames continue the sample sequence: indices accumulated.. (+spp)
         make_jitter(g.accumulated, g.desc.samples_per_pixel, g.jitter_host);
@@ -586,7 +601,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.material = g.d_material;
         p.jitter = g.d_jitter;
         p.out = g.d_fb;
-        p.partial = g.d_partial;
+        p.accum = g.d_accum;
         p.work = static_cast<uint32_t*>(g.d_counters);
         p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
         p.debug = static_cast<unsigned long long*>(g.d_debug);
@@ -614,45 +629,49 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.chunk = g.chunk;
         p.nchunks = g.nchunks;
         p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
-                  (slab ? vcrt::kFlagSlab : 0u);
+                  (g.direct ? vcrt::kFlagDirect : 0u);
+        p.spp_total = static_cast<float>(spp_total);
         const std::array<float, 12> cam = camera_array();
         for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
         // scan table: (groups + 1 padding group) x 64 B
         const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
         // per-lane culled scan: tables in LDS. Up to 32 KB with 256-thread workgroups (5 per
         // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
-        // copy for 16 waves); beyond that from global memory.
+        // copy for 16 waves); beyond that from global memory. Every kernel also keeps its waves'
+        // sample sums in LDS (kWaveAccumBytes per wave, ahead of the tables).
+        const uint32_t acc4 = 0, acc16 = 0;
         const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
         const uint32_t tab_lds_flat =
             static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 5));  // cbound_nf
-        const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
-        const bool lane_wide = lane_lds && tab_lds > 32768u;
+        const bool lane_lds = tab_lds + acc16 <= g.max_lds && g.cull_lane_tables != 2;
+        const bool lane_wide = lane_lds && tab_lds + acc4 > 32768u;
         int variant = g.desc.kernel_variant;
         // Measured on MI355X (1080p, box hierarchy): of the linear scans the scalar-cache
         // variant (sphere data in SGPRs, no LDS traffic) beats LDS staging by 15% (485
         // spheres) and 18% (4100); the culled scans beat both (same bits). AUTO: the flattened
-        // scan when its tables fit in LDS beside its stacks (485 spheres: 3.3x SMEM, +14%
-        // over CULL_LANE, +28% over CULL), else the per-lane scan (4100 spheres, 1024-thread
-        // blocks: 6.2x SMEM, level with CULL), and SMEM when the scene has no tables (< 16
-        // spheres or unbounded).
+        // scan (485 spheres: 3.3x SMEM, +14% over CULL_LANE, +28% over CULL; 4100 spheres with
+        // its tables in global memory), and SMEM when the scene has no tables (< 16 spheres or
+        // unbounded).
         if (variant == VCRT_KERNEL_AUTO)
             variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_FLAT;
-        if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
+        if (variant == VCRT_KERNEL_LDS && geom_lds + acc4 > g.max_lds) variant = VCRT_KERNEL_SMEM;
         if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE ||
              variant == VCRT_KERNEL_CULL_FLAT) &&
             g.ncgroups == 0)
             variant = VCRT_KERNEL_SMEM;
-        // the flat scan keeps 4 KB of stacks per wave in LDS (4 waves per block), beside its
-        // tables when they fit in 32 KB (16-bit entries); otherwise the tables stay in global
-        // memory and the stacks take 32-bit entries (6.25 KB per wave)
+        // The flat scan keeps 4 KB of stacks per wave in LDS beside its tables when they fit in
+        // 32 KB (16-bit entries), in 640-thread workgroups: two per CU (20 waves) share two
+        // copies of the tables, where five 256-thread workgroups would need five. Otherwise the
+        // tables stay in global memory and the stacks take 32-bit entries (6.25 KB per wave).
         const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
                               g.ncgroups <= vcrt::kFlatMaxGroups;
         hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
-        uint32_t lds = 0;
+        uint32_t block = 256;
+        uint32_t lds = acc4;
         if (variant == VCRT_KERNEL_LDS) {
             f = g.k_trace_lds;
             fs = g.k_trace_lds_stats;
-            lds = geom_lds;
+            lds = acc4 + geom_lds;
         } else if (variant == VCRT_KERNEL_CULL) {
             f = g.k_trace_cull;
             fs = g.k_trace_cull_stats;
@@ -667,17 +686,17 @@ vcrt_result vcrt_draw_next_frame(void) {
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
             f = g.k_trace_cull_lane_lds_wide;
             fs = g.k_trace_cull_lane_lds_wide_stats;
-            lds = tab_lds;
+            block = 1024;
+            lds = acc16 + tab_lds;
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_lds) {
             f = g.k_trace_cull_lane_lds;
             fs = g.k_trace_cull_lane_lds_stats;
-            lds = tab_lds;
+            lds = acc4 + tab_lds;
         } else if (variant == VCRT_KERNEL_CULL_LANE) {
             f = g.k_trace_cull_lane;
             fs = g.k_trace_cull_lane_stats;
         }
         if (g.debug_stats) f = fs;
-        const uint32_t block = (variant == VCRT_KERNEL_CULL_LANE && lane_wide) ? 1024 : 256;
         int per_cu = g.desc.blocks_per_cu;
         if (per_cu <= 0) {
             per_cu = 0;
@@ -688,6 +707,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         }
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
         VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
+        if (!g.direct && !g.desc.progressive)  // every frame sums from zero
+            VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
         if (g.debug_stats) {
             unsigned long long init[24] = {0, 0, 0, 0, 0, ~0ull};
             VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
@@ -697,12 +718,10 @@ vcrt_result vcrt_draw_next_frame(void) {
         VkResult r = launch(f, grid, block, lds, p);
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
-        if (slab) {
-            const float spp_total =
-                static_cast<float>(g.accumulated + static_cast<uint64_t>(g.desc.samples_per_pixel));
-            vcrt::ResolveParams rp{g.d_partial,   g.d_fb,      g.d_accum,     spp_total,
-                                   g.desc.width,  g.desc.height, g.desc.rank, g.desc.world_size,
-                                   g.tiles_x,     g.local_tiles, g.nchunks,   g.desc.samples_per_pixel};
+        if (!g.direct) {
+            vcrt::ResolveParams rp{g.d_accum,     g.d_fb,        static_cast<float>(spp_total),
+                                   g.desc.width,  g.desc.height, g.desc.rank,
+                                   g.desc.world_size, g.tiles_x, g.local_tiles};
             const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
             r = launch(g.k_resolve, rgrid, 256, 0, rp);
             if (r != VK_SUCCESS) return r;
@@ -715,7 +734,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         float ms = 0.f;
         VCRT_TRY(hipEventElapsedTime(&ms, g.ev_start, g.ev_stop));
         g.stats.kernel_ms = ms;
-        if (slab) {
+        if (!g.direct) {
             VCRT_TRY(hipEventElapsedTime(&ms, g.ev_stop, g.ev_resolve));
             g.stats.resolve_ms = ms;
         }
@@ -758,7 +777,6 @@ vcrt_result vcrt_end(void) {
     if (g.ev_start) (void)hipEventDestroy(g.ev_start);
     if (g.ev_stop) (void)hipEventDestroy(g.ev_stop);
     if (g.ev_resolve) (void)hipEventDestroy(g.ev_resolve);
-    if (g.d_partial) (void)hipFree(g.d_partial);
     if (g.d_accum) (void)hipFree(g.d_accum);
     if (g.d_srgb_thresholds) (void)hipFree(g.d_srgb_thresholds);
     if (g.d_srgb) (void)hipFree(g.d_srgb);
@@ -825,7 +843,7 @@ vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width
 vcrt_result vcrt_reset_accumulation(void) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     VCRT_TRY(hipStreamSynchronize(g.stream));
-    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, sizeof(float4) * g.total_pixels));
+    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
     g.accumulated = 0;
     make_jitter(0, g.desc.samples_per_pixel, g.jitter_host);
     VCRT_TRY(hipMemcpy(g.d_jitter, g.jitter_host.data(), sizeof(float2) * g.jitter_host.size(),

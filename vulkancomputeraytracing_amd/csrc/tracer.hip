@@ -12,9 +12,10 @@
 //   * Work items are (8x8 pixel tile, chunk of K samples, slot): one lane per pixel, the
 //     chunk's samples in order. A wave takes a whole block (one tile at one chunk = 64 items)
 //     with one atomic and hands its slots to lanes as they free up; a lane whose path ends
-//     starts its next sample at once (path regeneration). Chunk sums go to a [chunk][pixel]
-//     slab in HBM and vcrt_resolve adds them in chunk order (K >= spp: no slab, the
-//     reference's sequential sum).
+//     starts its next sample at once (path regeneration). An item's fp32 sum, quantized to
+//     2^-32, is added exactly to the pixel's sums (three f64 atomics; vcrt_math.h
+//     "Accumulation") and vcrt_resolve divides: the image depends on the chunk size only, not
+//     on the schedule or the number of GPUs. One item per pixel: the lane writes the pixel.
 //   * Ray state lives in VGPRs. Sphere tests run two spheres per packed-fp32 instruction
 //     (v_pk_add_f32 / v_pk_mul_f32 on pair-SoA groups of four: 2 lane-ops per issue, the only
 //     way gfx950 reaches its fp32 peak).
@@ -1018,8 +1019,9 @@ __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, ui
 // kCull: 0 = linear scan (kLds: table in LDS), 1 = culled scan, 2 = per-lane culled scan
 // with the group tables copied to LDS, 3 = per-lane culled scan on global tables.
 template <bool kLds, bool kStats, int kCull = 0>
-__device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geom) {
+__device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn) {
     const int n = p.nspheres;
+    float4* const lds_geom = lds_dyn;
     if constexpr (kLds) {
         const int nq = 4 * (((n + 3) >> 2) + 1);
         for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = p.geom[i];
@@ -1050,14 +1052,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
     const f3 du = mk(p.cam[3], p.cam[4], p.cam[5]);
     const f3 dv = mk(p.cam[6], p.cam[7], p.cam[8]);
     const f3 cam = mk(p.cam[9], p.cam[10], p.cam[11]);
-    const float spp_f = (float)p.spp;
     const uint32_t nchunks = (uint32_t)p.nchunks;
     const bool reverse = (p.flags & kFlagReverseOrder) != 0;
 
     bool done = false, need = true;
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
     int sample = 0, sample_end = 0, pass = 0;
-    uint32_t q = 0, chunk = 0, out_index = 0;
+    uint32_t q = 0;
+    uint32_t pxy = 0;  // the item's pixel: y << 16 | x
     f3 pc = mk(0.f, 0.f, 0.f), o = pc, d = pc, atten = pc, acc = pc;
     unsigned long long segs = 0;
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
@@ -1139,15 +1141,28 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
         }
 
         if (ended) {
-            acc = add(acc, contrib);
+            acc = add(acc, contrib);  // the chunk's fp32 sum in sample order
             ++sample;
             if (sample == sample_end) {
-                if ((p.flags & kFlagSlab) == 0u)
-                    p.out[out_index] =
-                        make_float4(acc.x / spp_f, acc.y / spp_f, acc.z / spp_f, 1.0f);
-                else
-                    p.partial[(size_t)chunk * (p.local_tiles * 64u) + q] =
-                        make_float4(acc.x, acc.y, acc.z, 0.0f);
+                if ((p.flags & kFlagDirect) != 0u) {
+                    // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
+                    const uint32_t out_index =
+                        p.world == 1 ? (pxy >> 16) * (uint32_t)p.width + (pxy & 0xffffu) : q;
+                    p.out[out_index] = make_float4(acc.x / p.spp_total, acc.y / p.spp_total,
+                                                   acc.z / p.spp_total, 1.0f);
+                } else {
+                    // the chunk sum, quantized: RN_even(S * 2^32) (an integer below 2^44),
+                    // summed exactly over the pixel's chunks in double; |S| >= 2^12, inf or NaN
+                    // make the pixel NaN (vcrt_math.h "Accumulation")
+                    const float amax = fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fabsf(acc.z));
+                    const bool ok = amax < kAccumLimit && acc.x == acc.x && acc.y == acc.y &&
+                                    acc.z == acc.z;
+                    const double nan = __builtin_nan("");
+                    double* s = p.accum + 4u * q;
+                    atomicAdd(s + 0, ok ? (double)__builtin_rintf(acc.x * kAccumScale) : nan);
+                    atomicAdd(s + 1, ok ? (double)__builtin_rintf(acc.y * kAccumScale) : nan);
+                    atomicAdd(s + 2, ok ? (double)__builtin_rintf(acc.z * kAccumScale) : nan);
+                }
                 need = true;
             } else {
                 const float2 jt = p.jitter[sample];
@@ -1209,13 +1224,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_geo
             need_mask = __ballot(need && !done);
         }
         if (got) {
-            chunk = g_chunk;
             q = g_lt * 64u + g_slot;
-            out_index = p.world == 1 ? g_py * (uint32_t)p.width + g_px : q;
+            pxy = (g_py << 16) | g_px;
             // shader.comp:43  pixel00 + x*delta_u + y*delta_v
             pc = add(add(p00, scale((float)g_px, du)), scale((float)g_py, dv));
             acc = mk(0.f, 0.f, 0.f);
-            sample = (int)(chunk * (uint32_t)p.chunk);
+            sample = (int)(g_chunk * (uint32_t)p.chunk);
             sample_end = min(sample + p.chunk, p.spp);
             // first camera ray of the chunk, shader.comp:48-52
             const float2 jt = p.jitter[sample];
@@ -1390,16 +1404,19 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_lds(TraceParams p) 
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem(TraceParams p) {
-    trace_impl<false, false>(p, nullptr);
+    extern __shared__ __attribute__((aligned(16))) float4 lds_dyn[];
+    trace_impl<false, false>(p, lds_dyn);
 }
 
 // Culled scan (exact; see scan_culled): spatially grouped sphere table + wave-level group tests.
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull(TraceParams p) {
-    trace_impl<false, false, 1>(p, nullptr);
+    extern __shared__ __attribute__((aligned(16))) float4 lds_dyn[];
+    trace_impl<false, false, 1>(p, lds_dyn);
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_stats(TraceParams p) {
-    trace_impl<false, true, 1>(p, nullptr);
+    extern __shared__ __attribute__((aligned(16))) float4 lds_dyn[];
+    trace_impl<false, true, 1>(p, lds_dyn);
 }
 
 // Per-lane culled scan (scan_culled_lane): tables in LDS (dynamic size = group-pair bounds +
@@ -1457,11 +1474,13 @@ extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_lane_lds_wide
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane(TraceParams p) {
-    trace_impl<false, false, 3>(p, nullptr);
+    extern __shared__ __attribute__((aligned(16))) float4 lds_dyn[];
+    trace_impl<false, false, 3>(p, lds_dyn);
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_stats(TraceParams p) {
-    trace_impl<false, true, 3>(p, nullptr);
+    extern __shared__ __attribute__((aligned(16))) float4 lds_dyn[];
+    trace_impl<false, true, 3>(p, lds_dyn);
 }
 
 // Diagnostics builds (VCRT_DEBUG_STATS=1): same kernels plus lane-occupancy/tail counters.
@@ -1471,27 +1490,22 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_lds_stats(TracePara
 }
 
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem_stats(TraceParams p) {
-    trace_impl<false, true>(p, nullptr);
+    extern __shared__ __attribute__((aligned(16))) float4 lds_dyn[];
+    trace_impl<false, true>(p, lds_dyn);
 }
 
-// Chunk sums -> pixels in chunk order: ((P0 + P1) + P2) + ..., then / spp (shader.comp:56).
+// Exact sample sums -> pixels (vcrt_math.h "Accumulation"; shader.comp:56 divides by SPP).
 extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) {
     const uint32_t elems = p.local_tiles * 64u;
+    const double st = (double)p.spp_total;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < elems;
          q += gridDim.x * blockDim.x) {
         const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
                                   (uint32_t)p.world, (uint32_t)p.rank);
         if (!px.valid) continue;
-        float4 s = p.accum ? p.accum[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int c = 0; c < p.nchunks; ++c) {  // 0 + P0 == P0: the first chunk is exact
-            const float4 v = p.partial[(size_t)c * elems + q];
-            s.x = s.x + v.x;
-            s.y = s.y + v.y;
-            s.z = s.z + v.z;
-        }
-        if (p.accum) p.accum[q] = s;
-        p.out[px.out_index] =
-            make_float4(s.x / p.spp_total, s.y / p.spp_total, s.z / p.spp_total, 1.0f);
+        const double4 s = *reinterpret_cast<const double4*>(p.accum + 4u * q);
+        p.out[px.out_index] = make_float4(resolve_channel(s.x, st), resolve_channel(s.y, st),
+                                          resolve_channel(s.z, st), 1.0f);
     }
 }
 

@@ -26,7 +26,8 @@ struct TraceParams {
     const float* material;        // [n] texture.x = material id
     const float2* jitter;  // [spp] (-0.5+rand(i,i), -0.5+rand(i+1,i+1)), shader.comp:48
     float4* out;           // rank-local framebuffer, rgba32f (layout above)
-    float4* partial;       // [nchunks][local_tiles * 64] chunk sums (nchunks > 1)
+    double* accum;         // [local_tiles * 64][4] exact sums of the quantized chunk sums (r, g,
+                           //   b, unused), vcrt_math.h "Accumulation"; unused with kFlagDirect
     uint32_t* work;        // work-item counter, zeroed before every launch
     unsigned long long* segments;  // ray segments traced, zeroed before every launch
     unsigned long long* debug;     // diagnostics counters (stats kernels only), may be null
@@ -57,27 +58,29 @@ struct TraceParams {
     uint32_t tiles_x;      // ceil(width / 8)
     uint32_t local_tiles;  // tiles owned by this rank
     uint32_t total_items;  // local_tiles * 64 * nchunks
-    int32_t chunk;         // samples per work item
+    int32_t chunk;         // samples per work item (<= kAccumMaxChunk)
     int32_t nchunks;       // ceil(spp / chunk)
     uint32_t flags;        // kFlag*
+    float spp_total;       // kFlagDirect: the divisor (samples per pixel)
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
 };
 
+constexpr uint32_t kFlatBlockThreads = 640;  // CULL_FLAT with LDS tables: 10 waves per workgroup
 constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
 constexpr uint32_t kWaveScratchBytes = 4096;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
 constexpr uint32_t kWaveScratchBytesWide = 6400;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
-constexpr uint32_t kFlagSlab = 4u;          // chunk sums always go to the slab (resolve pass)
+constexpr uint32_t kFlagDirect = 4u;  // one work item per pixel and frame, not progressive: the
+                                      // lane writes the pixel itself (no sums, no resolve pass)
 
+// Exact sums -> pixels (vcrt_math.h resolve_channel), rgba32f with alpha 1.
 struct ResolveParams {
-    const float4* partial;  // [nchunks][local_tiles * 64]
-    float4* out;            // rank-local framebuffer
-    float4* accum;          // progressive running sums [local_tiles * 64], or null
-    float spp_total;        // divisor: samples accumulated so far
+    const double* accum;              // [local_tiles * 64][4]
+    float4* out;                      // rank-local framebuffer
+    float spp_total;                  // samples per pixel accumulated so far (<= 2^19)
     int32_t width, height, rank, world;
     uint32_t tiles_x, local_tiles;
-    int32_t nchunks, spp;
 };
 
 struct AssembleParams {

@@ -302,6 +302,30 @@ VCRT_HD float schlick(float cosine, float ior) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Accumulation (shader.comp:46-56: color.rgb += ray_color(...); color /= SPP). The reference
+// sums a pixel's samples in fp32 in sample order. The GPU splits them into work items of K
+// samples (chunks, restarting at every progressive frame) and sums each chunk the same way.
+// One chunk per pixel (K >= spp, not progressive): color / SPP in fp32, the reference's
+// arithmetic exactly. Otherwise each chunk sum S is quantized to q = RN_even(S * 2^32) (the
+// scaling is exact; every fp32 S >= 2^-9 is kept exactly), the q are added in double -- exact,
+// as they are integers below 2^44 and a pixel has at most 512 chunks (< 2^53) -- and
+//     out = (float)((sum * 2^-32) / (double)spp_total).
+// Exact sums do not depend on the order of the additions, so the image is the same for any
+// schedule and any number of GPUs; it depends on K only, which defaults to a function of the
+// frame (width, height, spp). The quantized combination differs from the fp32 sequential sum
+// by less than that sum's own rounding error. A chunk sum with
+// |S| >= 2^12, inf or NaN makes the pixel NaN (the reference scenes' radiance is <= 1 per
+// sample).
+constexpr float kAccumScale = 0x1p32f;
+constexpr float kAccumLimit = 4096.0f;
+constexpr int32_t kAccumMaxChunks = 512;  // chunks per pixel (progressive frames included)
+
+// One channel of a pixel from the exact sum of its quantized chunk sums.
+VCRT_HD float resolve_channel(double s, double spp_total) {
+    return (float)((s * 0x1p-32) / spp_total);
+}
+
+// ---------------------------------------------------------------------------------------
 // Camera: shader.comp:18-39, computed once on the host (it is uniform per dispatch).
 
 struct Camera {

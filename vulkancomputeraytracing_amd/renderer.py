@@ -32,7 +32,7 @@ class RenderDesc:
     world_size: int = 1             # shards: rank owns the 8x8 tiles with (tx + ty) % world == rank
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
-    accumulate_chunk: int = 0       # 0 = 64 (halved for small jobs); >= spp: sequential order
+    accumulate_chunk: int = 0       # 0 = from the frame (work_chunk); >= spp: sequential order
     progressive: bool = False       # frame f continues the sample sequence; average of all frames
     code_object_path: str | None = None
     _path_keepalive: bytes | None = field(default=None, repr=False)
@@ -58,22 +58,10 @@ class RenderDesc:
         return d
 
 
-DEFAULT_ACCUMULATE_CHUNK = 64
-
-
-def effective_chunk(spp: int, accumulate_chunk: int = 0, pixels: int | None = None) -> int:
-    """Samples per work item the renderer uses (the oracle's `chunk` for the same order).
-    Mirrors default_chunk() in csrc/capi.cpp when accumulate_chunk is 0; `pixels` is the
-    largest rank's tile slots (64 per 8x8 tile: tile_slots(w, h) for one rank,
-    64 * distributed.tiles_per_rank(w, h, world) for a sharded frame)."""
-    if accumulate_chunk > 0:
-        k = accumulate_chunk
-    else:
-        k = DEFAULT_ACCUMULATE_CHUNK
-        if pixels is not None:
-            while k > 4 and pixels * (-(-spp // k)) < (1 << 24):
-                k //= 2
-    return min(k, spp)
+def work_chunk(desc: RenderDesc) -> int:
+    """Samples per work item (the accumulation chunk) the renderer uses for `desc`, from the
+    C ABI (vcrt_work_chunk: host only, no GPU). The oracle's `chunk` for the same image."""
+    return N.check_count("vcrt_work_chunk", N.lib().vcrt_work_chunk(ctypes.byref(desc.to_c())))
 
 
 def tiles_for_rank(width: int, height: int, world: int, rank: int) -> list[int]:
