@@ -1,24 +1,27 @@
 """Headline benchmark: Msamples/s (pixels x spp / s) rendering the RTIOW final scene at
 1920x1080, 1024 spp, max depth 10 (BASELINE.json metric, configs[3]) on N MI355X GPUs.
 
-One step = one DrawNextFrame of the whole frame: on every rank the gfx950 tracer renders the
-rank's 8x8 tiles (tile (tx, ty) belongs to rank (tx + ty) % N), then (N > 1) the packed rank
-framebuffers are all-gathered over RCCL and rank 0 re-interleaves the frame. The frame is fixed
-as N grows (strong scaling).
+One step = one DrawNextFrame of the whole frame. On every rank the gfx950 tracer renders the
+rank's 8x8 tiles (tile (tx, ty) belongs to rank (tx + ty) % N). For N > 1 the same
+vcrt_draw_next_frame then gathers every rank's packed tiles to rank 0 over RCCL, inside
+libvcrt.so (vcrt_comm_init; one grouped send/recv), and rank 0 re-interleaves the frame. The
+frame is fixed as N grows (strong scaling). torch.distributed (gloo) is only the control plane:
+the communicator id, barriers and the max-over-ranks time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
        torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector, MI355X_MICROARCH.md chip table
+PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector (packed FMA), MI355X_MICROARCH.md chip table
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
 FLOPS_PER_BOUND_TEST = 26       # tracer.hip box_gap, per box: 6 fma 12, per-axis min/max 6,
                                 # tnear/tfar 4, gap sub + add + fma 4
@@ -58,8 +61,10 @@ def parse():
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--validate", action="store_true",
-                   help="rank 0 re-renders the frame on one GPU after the timed steps and checks "
-                        "the gathered frame bit for bit (use with an explicit --chunk)")
+                   help="after the timed steps, rank 0 checks its frame: bit for bit against the "
+                        "CPU oracle on a few rows at full spp, and (N > 1) against a 1-GPU "
+                        "render of the whole frame")
+    p.add_argument("--validate-rows", type=int, default=2)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU work for the cpu_baseline sample")
     a = p.parse_args()
@@ -69,12 +74,55 @@ def parse():
     return a
 
 
+# ---- host description (cpu_baseline) ---------------------------------------------------------
+
+def cpu_quota():
+    """CPUs this process may use: its affinity set, capped by a cgroup v2/v1 CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(period))))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                n = min(n, max(1, q // period))
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def host_cpu():
+    """Model name and physical core count of the host (all sockets), from /proc/cpuinfo."""
+    model, cores = platform.processor() or "?", set()
+    phys = core = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None and core is not None:
+                cores.add((phys, core))
+                phys = core = None
+    except OSError:
+        pass
+    return model, (len(cores) or None)
+
+
 def cpu_baseline(args):
-    """The CPU oracle (C restatement of shader.comp) on a bounded sample of the same workload:
-    full-width rows y = 0, k, 2k, ... at the first s samples, on the host's cores."""
+    """The CPU oracle (C restatement of shader.comp, oracle/vcrt_oracle.c -O3) on a bounded
+    sample of the same workload: full-width rows y = 0, k, 2k, ... (or the whole frame at the
+    first s samples), on every CPU this process may use."""
     from tests import oracle_py
     o = oracle_py.load()
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_quota()
     scene = o.scene(args.scene)
     # calibrate on a tiny sample, then size the real one for ~cpu_seconds of work
     # (34 rows spread over the frame: sky, spheres and ground in frame proportion)
@@ -99,12 +147,47 @@ def cpu_baseline(args):
     o.render(o.config(args.width, args.height, spp, args.depth), scene, rows=rows, threads=threads)
     dt = time.perf_counter() - t0
     samples = len(rows) * args.width * spp
+    model, phys = host_cpu()
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/vcrt_oracle.c -O3, {threads} threads: rows y%{step}==0 "
-                      f"({len(rows)} rows x {args.width}) at spp {spp} of the same "
-                      f"{args.scene} scene/camera/depth {args.depth}; {samples} samples "
-                      f"in {dt:.2f} s",
+            "threads": threads, "host_logical_cpus": os.cpu_count(),
+            "host_physical_cores": phys, "cpu_model": model,
+            "sample": f"oracle/vcrt_oracle.c -O3 (linear hit_sphere scan, the reference's "
+                      f"algorithm), {threads} threads = every CPU this job may use (affinity "
+                      f"and cgroup quota; the host has {os.cpu_count()} logical CPUs): rows "
+                      f"y%{step}==0 ({len(rows)} rows x {args.width}) at spp {spp} of the same "
+                      f"{args.scene} scene/camera/depth {args.depth}; {samples} samples in "
+                      f"{dt:.2f} s",
             "seconds": round(dt, 3)}
+
+
+# ---- validation (outside the timed region) ---------------------------------------------------
+
+def validate(args, got, st, device, world):
+    """Rank 0's frame against the CPU oracle on a few full-width rows at full spp and depth
+    (bit for bit, same accumulation chunk), and for N > 1 against a 1-GPU render."""
+    import numpy as np
+    from tests import oracle_py
+    import vulkancomputeraytracing_amd as vc
+    o = oracle_py.load()
+    out = {}
+    rows = list(range(args.height // (2 * args.validate_rows), args.height,
+                      max(1, args.height // args.validate_rows)))[:args.validate_rows]
+    cfg = o.config(args.width, args.height, args.spp, args.depth, chunk=st["accumulate_chunk"])
+    want = np.stack([o.render(cfg, o.scene(args.scene), rows=range(y, y + 1), threads=cpu_quota())[0][y]
+                     for y in rows])
+    out["rows_vs_oracle"] = rows
+    out["bitwise_vs_oracle"] = bool(np.array_equal(got[rows].view(np.uint32),
+                                                   want.view(np.uint32)))
+    if world > 1:
+        ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
+                                 max_depth=args.depth, device=device, kernel_variant=args.variant,
+                                 accumulate_chunk=args.chunk)
+        with vc.Renderer(ref_desc, args.scene) as ref:
+            ref.draw_next_frame()
+            one = ref.read_framebuffer()
+        out["bitwise_vs_1gpu"] = bool(np.array_equal(got.view(np.uint32), one.view(np.uint32)))
+    log(f"validate: {out}")
+    return out
 
 
 def main():
@@ -120,36 +203,40 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    # one process per GPU; VCRT_DIST_BACKEND=gloo rehearses the N > 1 flow with several ranks
-    # sharing the GPUs of a smaller box (RCCL needs one GPU per rank)
+    # One process per GPU. The frame gather runs over RCCL inside libvcrt (vcrt_comm_init).
+    # VCRT_DIST_BACKEND=gloo rehearses the N > 1 flow with several ranks sharing the GPUs of a
+    # smaller box (RCCL needs one GPU per rank): the gather then goes through gloo.
     backend = os.environ.get("VCRT_DIST_BACKEND", "nccl")
     device = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")  # control plane: comm id, barriers, max time
 
     desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
                          max_depth=args.depth, device=device, rank=rank, world_size=world,
                          kernel_variant=args.variant,
                          blocks_per_cu=args.blocks_per_cu, accumulate_chunk=args.chunk)
-    dev = torch.device("cuda", device)
-    tiles_pad = D.tiles_per_rank(args.width, args.height, world)
-    local_elems = args.width * args.height if world == 1 else tiles_pad * 64
-    local = torch.zeros((local_elems, 4), dtype=torch.float32, device=dev)
-    frame = None
-    if world > 1 and rank == 0:
-        frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
-
     r = vc.Renderer(desc, args.scene)
-    r.set_framebuffer_device(local.data_ptr(), local.numel() * 4)
     nspheres = len(vc.builtin_scene(args.scene))
+    gather = None
+    frame = local = None
+    if world > 1 and backend == "nccl":
+        ids = [vc.renderer.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        r.comm_init(ids[0])
+        gather = "rccl in libvcrt (vcrt_draw_next_frame: grouped send/recv to rank 0)"
+    elif world > 1:
+        dev = torch.device("cuda", device)
+        tiles_pad = D.tiles_per_rank(args.width, args.height, world)
+        local = torch.zeros((tiles_pad * 64, 4), dtype=torch.float32, device=dev)
+        r.set_framebuffer_device(local.data_ptr(), local.numel() * 4)
+        if rank == 0:
+            frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
+        gather = "gloo rehearsal (torch.distributed.gather of host copies)"
 
     def step():
-        r.draw_next_frame()  # returns when the rank's rows are complete
-        if world > 1:
+        r.draw_next_frame()  # N > 1 (RCCL): returns on rank 0 with the gathered frame
+        if local is not None:
             gathered = D.gather_tiles(local, tiles_pad)
             if rank == 0:
                 torch.cuda.current_stream().synchronize()
@@ -164,7 +251,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    kernel_ms, segments = [], []
+    kernel_ms, segments, gather_ms = [], [], []
     barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -172,55 +259,49 @@ def main():
         st = r.stats()
         kernel_ms.append(st["kernel_ms"])
         segments.append(st["segments"])
+        gather_ms.append(st["gather_ms"])
         log(f"[rank {rank}] step {i}: frame {st['frame_ms']:.1f} ms, kernel "
-            f"{st['kernel_ms']:.1f} ms, {st['segments']} segments")
+            f"{st['kernel_ms']:.1f} ms, gather {st['gather_ms']:.2f} ms, "
+            f"{st['segments']} segments")
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = r.stats()
-    r.close()
     validated = None
     if args.validate and rank == 0:
-        import numpy as np
-        got = (frame if world > 1 else local.view(args.height, args.width, 4)).cpu().numpy()
-        # the reference render sums in the ranks' chunks (the default chunk follows the largest
-        # rank's share, so it is the same on every rank)
-        ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
-                                 max_depth=args.depth, device=device, kernel_variant=args.variant,
-                                 accumulate_chunk=st["accumulate_chunk"])
-        with vc.Renderer(ref_desc, args.scene) as ref:
-            ref.draw_next_frame()
-            want = ref.read_framebuffer()
-        validated = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
-        log(f"validate: gathered frame bit-identical to a 1-GPU render: {validated}")
+        if frame is not None:
+            got = frame.cpu().numpy()
+        else:
+            got = r.read_framebuffer()
+        validated = validate(args, got, st, device, world)
+    r.close()
 
     if rank == 0:
         samples = args.width * args.height * args.spp * args.steps
         value = samples / elapsed / 1e6
         k_ms = sum(kernel_ms) / len(kernel_ms)
         seg = sum(segments) / len(segments)
-        # Algorithmic work: the reference's linear scan tests every sphere on
-        # every segment, 23 flops each (functions.glsl:15-19).
-        flops = seg * nspheres * FLOPS_PER_SPHERE_TEST
-        # Issued work: the culled scans skip most of those tests (same bits): every lane of each
-        # wave-level group test (4 spheres x 23) and box test (26); the linear scans issue all.
-        executed = flops
-        if st["kernel_variant"] in (3, 4, 5):
-            executed = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
-                        + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
         kernel = KERNEL_NAMES.get(st["kernel_variant"], "?")
         if st["kernel_variant"] == 4 and st["tables_in_lds"]:
             kernel += "_lds_wide" if st["block_threads"] == 1024 else "_lds"
         if st["kernel_variant"] == 5 and not st["tables_in_lds"]:
             kernel += "_global"
-        achieved = flops / (k_ms * 1e-3) / 1e12
-        issued = executed / (k_ms * 1e-3) / 1e12
-        # HBM bytes and VALU busy of the same kernel at this config, from the committed
-        # rocprofv3 PMC passes (tools/gpu_profile.sh -> profiles/traffic.json)
+        # Issued work of the timed kernel (the roofline numerator): every lane of each
+        # wave-level exact group test (4 spheres x 23 flops, functions.glsl:15-19) and box test
+        # (26 flops), counted by in-kernel per-wave counters; the linear scans issue the
+        # reference's whole scan.
+        ref_flops = seg * nspheres * FLOPS_PER_SPHERE_TEST  # brute-force scan, SURVEY.md 8(d)
+        issued = ref_flops
+        if st["kernel_variant"] in (3, 4, 5):
+            issued = (st["group_tests"] * 64 * 4 * FLOPS_PER_SPHERE_TEST
+                      + st["bound_tests"] * 64 * FLOPS_PER_BOUND_TEST)
+        achieved = issued / (k_ms * 1e-3) / 1e12
+        # HBM bytes and VALU counters of this kernel at this workload, from the committed
+        # rocprofv3 PMC passes (tools/gpu_profile.sh -> profiles/traffic.json); used only when
+        # the profiled kernel is the one this run launched
         key = f"{args.scene}_{args.width}x{args.height}_s{args.spp}_d{args.depth}_n{world}"
         prof = {}
         if os.path.exists(PROFILE_TRAFFIC):
@@ -228,6 +309,8 @@ def main():
                 prof = json.load(open(PROFILE_TRAFFIC)).get(key, {})
             except (OSError, ValueError):
                 prof = {}
+        if prof.get("kernel") != kernel:
+            prof = {}
         cfg_name = next((n for n, c in CONFIGS.items()
                          if all(getattr(args, k) == v for k, v in c.items())), "custom")
         metric = ("Msamples/sec (pixels×spp/s) at 1920×1080, 1024spp, RTIOW final scene"
@@ -252,33 +335,35 @@ def main():
                        "scene": args.scene, "spheres": nspheres, "width": args.width,
                        "height": args.height, "spp": args.spp, "max_depth": args.depth,
                        "parallelism": f"tiles8x8-diagonal-x{world}",
+                       "gather": gather,
                        "accumulate_chunk": st["accumulate_chunk"],
                        "kernel_variant": st["kernel_variant"],
                        "grid_blocks": st["grid_blocks"]},
-            # fp32 VALU-bound (no MFMA); achieved = algorithmic flops per
-            # launch (segments x spheres x 23, the reference's hit_sphere scan of every
-            # segment this launch traced) / the kernel's HIP-event time. The exact culled
-            # scan skips most of those tests with bit-identical results, so frac exceeds 1;
-            # what the kernel issued is beside it, and the hardware view is VALU busy.
+            # fp32 VALU-bound (no MFMA). achieved = the fp32 work the timed
+            # kernel issued (exact sphere tests and box tests, per-wave counters) / its
+            # HIP-event time, so frac <= 1 is a roofline fraction. The brute-force equivalent
+            # (segments x spheres x 23: the reference's linear scan of every segment this
+            # launch traced) is reported as a speed-up beside it.
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": prof.get("hbm_bytes_per_launch"),
                          "kernel": kernel, "kernel_ms": round(k_ms, 3),
-                         "numerator": "SURVEY.md 8(d): segments x spheres x 23 flops per launch "
-                                      "(functions.glsl:15-19 for every sphere of every segment)",
-                         "flops_per_launch": flops,
+                         "numerator": "issued fp32 work per launch: wave-level exact group "
+                                      "tests x 64 lanes x 4 x 23 + box tests x 64 x 26 "
+                                      "(in-kernel counters; DESIGN.md 7)",
+                         "issued_flops_per_launch": issued,
                          "segments_per_launch": int(seg),
-                         "issued_flops_per_launch": executed,
-                         "issued_tflops": round(issued, 3),
-                         "issued_frac": round(issued / PEAK_FP32_TFLOPS, 4),
-                         "issued_numerator": "wave-level group tests x 64 x 4 x 23 + bound tests "
-                                             "x 64 x 26 (DESIGN.md 5)",
-                         "valu_busy_pct": prof.get("valu_busy_pct"),
-                         "valu_utilization_pct": prof.get("valu_utilization_pct")},
+                         "bruteforce_flops_per_launch": ref_flops,
+                         "speedup_vs_bruteforce_at_peak": round(
+                             ref_flops / (PEAK_FP32_TFLOPS * 1e12) / (k_ms * 1e-3), 3),
+                         "valu_issue_frac": prof.get("valu_issue_frac"),
+                         "valu_lane_util": prof.get("valu_lane_util"),
+                         "profile": prof.get("source")},
+            "gather_ms": round(sum(gather_ms) / len(gather_ms), 3),
         }
         if validated is not None:
-            out["validated_bitwise_vs_1gpu"] = validated
+            out["validated"] = validated
         if world == 1 and not args.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(args)

@@ -116,6 +116,7 @@ typedef struct vcrt_stats {
     double kernel_ms;      /* tracer kernel time, HIP events on the render stream */
     double frame_ms;       /* host wall time of the last vcrt_draw_next_frame */
     double resolve_ms;     /* resolve kernel time (exact chunk sums -> pixels; 0: one chunk) */
+    double gather_ms;      /* multi-GPU frame gather + re-interleave (vcrt_comm_init), HIP events */
     int32_t frames;        /* frames drawn since vcrt_begin */
     int32_t grid_blocks, block_threads, kernel_variant;
     int32_t local_tiles;   /* 8x8 tiles this rank renders */
@@ -151,6 +152,21 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count);
 vcrt_result vcrt_draw_next_frame(void);
 vcrt_result vcrt_end(void);
 
+/* Multi-GPU, one process per GPU (the reference renders on one GPU: Environment.cpp:157-165;
+ * "TODO: Cross-GPU sharing", Frontend.cpp:107). Each process calls vcrt_begin with its rank,
+ * world_size and device, then vcrt_comm_init with the same id on every rank (rank 0 makes it
+ * with vcrt_comm_unique_id and hands it out, e.g. over a TCP store). From then on
+ * vcrt_draw_next_frame renders the rank's tiles and gathers every rank's packed tiles to rank 0
+ * over RCCL (one grouped send/recv) and re-interleaves them there: on rank 0 it returns with the
+ * whole frame, which vcrt_read_framebuffer / vcrt_framebuffer_device then give as [height][width]
+ * (the other ranks keep their packed tiles). Collective: every rank must draw every frame.
+ * vcrt_end destroys the communicator. */
+typedef struct vcrt_comm_id {
+    char internal[128]; /* an ncclUniqueId */
+} vcrt_comm_id;
+vcrt_result vcrt_comm_unique_id(vcrt_comm_id* id);
+vcrt_result vcrt_comm_init(const vcrt_comm_id* id);
+
 /* Rank-local framebuffer layout. world_size == 1: the frame, row-major [height][width] (row 0 =
  * top, as the reference's storage image). world_size > 1: packed tiles [tiles][64] with element
  * 8*(y%8) + x%8 of each tile (pixels outside the frame in edge tiles are left untouched). */
@@ -158,9 +174,10 @@ vcrt_result vcrt_local_layout(uint32_t* elements, uint32_t* tiles);
 /* Copies the rank-local framebuffer (elements * 4 floats, rgba32f) to host memory; count = number
  * of floats available at rgba. */
 vcrt_result vcrt_read_framebuffer(float* rgba, size_t count);
-/* Device address and size of the rank-local framebuffer (for collectives). */
+/* Device address and size of the framebuffer vcrt_read_framebuffer reads. */
 vcrt_result vcrt_framebuffer_device(void** device_ptr, size_t* bytes);
-/* Render into caller-owned device memory (>= elements*16 bytes, 16-B aligned); NULL = own. */
+/* Render into caller-owned device memory (>= elements*16 bytes, 16-B aligned); NULL = own.
+ * VK_ERROR_FEATURE_NOT_PRESENT after vcrt_comm_init (the gather owns the buffers). */
 vcrt_result vcrt_set_framebuffer_device(void* device_ptr, size_t bytes);
 /* Rebuild the frame from gathered rank framebuffers: gathered = [world][tiles_per_rank][64]
  * float4 (rank-major, each rank's packed tiles padded to tiles_per_rank), frame = [height][width]

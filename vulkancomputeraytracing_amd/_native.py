@@ -87,6 +87,7 @@ class vcrt_stats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("frame_ms", ctypes.c_double),
         ("resolve_ms", ctypes.c_double),
+        ("gather_ms", ctypes.c_double),
         ("frames", ctypes.c_int32),
         ("grid_blocks", ctypes.c_int32),
         ("block_threads", ctypes.c_int32),
@@ -103,6 +104,10 @@ class vcrt_stats(ctypes.Structure):
     ]
 
 
+class vcrt_comm_id(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]  # an ncclUniqueId
+
+
 # name -> (restype, argtypes); every symbol include/vcrt.h declares.
 SIGNATURES = {
     "vcrt_default_desc": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
@@ -111,6 +116,8 @@ SIGNATURES = {
     "vcrt_set_scene": (ctypes.c_int32, [ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_draw_next_frame": (ctypes.c_int32, []),
     "vcrt_end": (ctypes.c_int32, []),
+    "vcrt_comm_unique_id": (ctypes.c_int32, [ctypes.POINTER(vcrt_comm_id)]),
+    "vcrt_comm_init": (ctypes.c_int32, [ctypes.POINTER(vcrt_comm_id)]),
     "vcrt_local_layout": (ctypes.c_int32, [ctypes.POINTER(ctypes.c_uint32),
                                            ctypes.POINTER(ctypes.c_uint32)]),
     "vcrt_read_framebuffer": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_size_t]),
@@ -155,9 +162,12 @@ def _share_torch_hip_runtime() -> None:
         import torch  # noqa: F401
     except ImportError:
         return
-    torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
-    if os.path.exists(torch_lib):
-        ctypes.CDLL(torch_lib, mode=ctypes.RTLD_GLOBAL)
+    # the same for RCCL (SONAME librccl.so.1 in both): libvcrt's gather and torch's
+    # process group then use one RCCL
+    for name in ("libamdhip64.so", "librccl.so"):
+        torch_lib = os.path.join(os.path.dirname(torch.__file__), "lib", name)
+        if os.path.exists(torch_lib):
+            ctypes.CDLL(torch_lib, mode=ctypes.RTLD_GLOBAL)
 
 
 def lib() -> ctypes.CDLL:

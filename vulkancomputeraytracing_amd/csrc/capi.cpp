@@ -19,6 +19,7 @@
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
 #include "Shader.hpp"
 #include "cluster.hpp"
@@ -94,6 +95,13 @@ struct RendererState {
     uint32_t tiles_x = 0, local_tiles = 0;
     uint32_t local_elems = 0;   // float4 elements of the rank-local framebuffer
     uint64_t local_pixels = 0;  // frame pixels this rank renders
+    uint32_t pad_tiles = 0;     // tiles of the largest rank: the packed framebuffers' size
+    // multi-GPU, one process per GPU (vcrt_comm_init): the ranks' packed framebuffers go to
+    // rank 0 in one grouped RCCL send/recv inside vcrt_draw_next_frame; rank 0 assembles them
+    ncclComm_t comm = nullptr;
+    float4* d_gather = nullptr;  // rank 0: [world][pad_tiles][64], its own tiles in slot 0
+    float4* d_frame = nullptr;   // rank 0: the assembled frame [height][width]
+    hipEvent_t ev_gather_start = nullptr, ev_gather = nullptr;
     vcrt::Camera cam{};
     vcrt_stats stats{};
 };
@@ -300,10 +308,63 @@ bool desc_valid(const vcrt_render_desc& d) {
     return true;
 }
 
+// The framebuffer the caller sees: rank 0 of a gathering communicator holds the assembled
+// frame [height][width]; otherwise the rank-local framebuffer.
+struct FbView {
+    float4* ptr;
+    uint32_t elems;
+};
+FbView fb_view() {
+    if (g.d_frame)
+        return {g.d_frame, static_cast<uint32_t>(g.desc.width) * static_cast<uint32_t>(g.desc.height)};
+    return {g.d_fb, g.local_elems};
+}
+
+VkResult nccl_vk(ncclResult_t e) {
+    if (e == ncclSuccess) return VK_SUCCESS;
+    if (e == ncclSystemError || e == ncclRemoteError) return VK_ERROR_DEVICE_LOST;
+    return e == ncclInvalidArgument || e == ncclInvalidUsage ? VK_ERROR_INITIALIZATION_FAILED
+                                                             : VK_ERROR_UNKNOWN;
+}
+
 template <typename Params>
 VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Params& params) {
     void* args[] = {&params};
     VCRT_TRY(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, lds, g.stream, args, nullptr));
+    return VK_SUCCESS;
+}
+
+// The frame gather, stream-ordered after the trace and resolve: every rank's
+// packed tiles (pad_tiles x 64 float4, 4.1 MB per rank at 1080p / 8 GPUs) go to rank 0 in one
+// grouped send/recv, so rank 0 receives from all peers at once over their own xGMI links
+// (a ring all-gather would move the whole frame through every rank); rank 0 then
+// re-interleaves the frame (vcrt_assemble). Every rank takes part, whatever its share.
+VkResult gather_frame() {
+    VCRT_TRY(hipEventRecord(g.ev_gather_start, g.stream));
+    const size_t n = static_cast<size_t>(g.pad_tiles) * 64 * 4;  // floats per rank
+    VkResult r = nccl_vk(ncclGroupStart());
+    if (r != VK_SUCCESS) return r;
+    if (g.desc.rank == 0) {
+        for (int32_t peer = 1; peer < g.desc.world_size && r == VK_SUCCESS; peer++)
+            r = nccl_vk(ncclRecv(reinterpret_cast<float*>(g.d_gather) + n * peer, n,
+                                 ncclFloat32, peer, g.comm, g.stream));
+    } else {
+        r = nccl_vk(ncclSend(g.d_fb, n, ncclFloat32, 0, g.comm, g.stream));
+    }
+    const VkResult r_end = nccl_vk(ncclGroupEnd());
+    if (r != VK_SUCCESS) return r;
+    if (r_end != VK_SUCCESS) return r_end;
+    if (g.desc.rank == 0) {
+        vcrt::AssembleParams ap{g.d_gather,    g.d_frame,         g.desc.width,
+                                g.desc.height, g.desc.world_size, g.tiles_x,
+                                g.pad_tiles};
+        const uint64_t total = static_cast<uint64_t>(g.desc.width) * g.desc.height;
+        r = launch(g.k_assemble,
+                   static_cast<uint32_t>(std::min<uint64_t>((total + 255) / 256, 8192)), 256, 0,
+                   ap);
+        if (r != VK_SUCCESS) return r;
+    }
+    VCRT_TRY(hipEventRecord(g.ev_gather, g.stream));
     return VK_SUCCESS;
 }
 
@@ -405,6 +466,9 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
                         ? static_cast<uint32_t>(g.desc.width) * static_cast<uint32_t>(g.desc.height)
                         : g.local_tiles * 64u;
     g.fb_bytes = static_cast<size_t>(g.local_elems) * sizeof(float4);
+    for (int32_t rr = 0; rr < g.desc.world_size; rr++)
+        g.pad_tiles = std::max(g.pad_tiles, tiles_for_rank(g.desc.width, g.desc.height,
+                                                           g.desc.world_size, rr));
     for (uint32_t lt = 0; lt < g.local_tiles; lt++) {
         uint32_t tx, ty;
         vcrt::tile_of(lt, static_cast<uint32_t>(g.desc.rank),
@@ -412,9 +476,11 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         g.local_pixels += std::min<uint64_t>(8, g.desc.width - 8 * tx) *
                           std::min<uint64_t>(8, g.desc.height - 8 * ty);
     }
-    if (g.fb_bytes) {
-        if ((r = to_vk(hipMalloc(&g.d_fb_own, g.fb_bytes))) != VK_SUCCESS) return fail(r);
-        if ((r = to_vk(hipMemset(g.d_fb_own, 0, g.fb_bytes))) != VK_SUCCESS) return fail(r);
+    if (g.fb_bytes) {  // sharded: padded to the largest rank, the size every rank sends
+        const size_t own = g.desc.world_size == 1 ? g.fb_bytes
+                                                  : static_cast<size_t>(g.pad_tiles) * 64 * 16;
+        if ((r = to_vk(hipMalloc(&g.d_fb_own, own))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemset(g.d_fb_own, 0, own))) != VK_SUCCESS) return fail(r);
     }
     g.d_fb = g.d_fb_own;
     // Work decomposition: (local tile, chunk of K samples) items; a pixel's chunk sums are
@@ -570,6 +636,7 @@ vcrt_result vcrt_draw_next_frame(void) {
     g.stats.segments = 0;
     g.stats.kernel_ms = 0.0;
     g.stats.resolve_ms = 0.0;
+    g.stats.gather_ms = 0.0;
     if (pixels != 0 && g.desc.max_depth == 0) {
         // ray_color with MAX_RECURSION_LEVEL 0 returns its undefined value (canonical 0) for
         // every sample without scanning: the frame is (0,0,0,1).
@@ -751,6 +818,14 @@ vcrt_result vcrt_draw_next_frame(void) {
         g.stats.tables_in_lds = (f == g.k_trace_cull_flat || f == g.k_trace_cull_lane_lds ||
                                  f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
     }
+    if (g.comm && g.desc.world_size > 1) {
+        const VkResult r = gather_frame();
+        if (r != VK_SUCCESS) return r;
+        VCRT_TRY(hipStreamSynchronize(g.stream));
+        float ms = 0.f;
+        VCRT_TRY(hipEventElapsedTime(&ms, g.ev_gather_start, g.ev_gather));
+        g.stats.gather_ms = ms;
+    }
     VCRT_TRY(hipStreamSynchronize(g.stream));
     g.stats.sphere_tests = g.stats.segments * static_cast<uint64_t>(g.nspheres);
     g.stats.samples =
@@ -780,34 +855,81 @@ vcrt_result vcrt_end(void) {
     if (g.d_accum) (void)hipFree(g.d_accum);
     if (g.d_srgb_thresholds) (void)hipFree(g.d_srgb_thresholds);
     if (g.d_srgb) (void)hipFree(g.d_srgb);
+    if (g.comm) (void)ncclCommDestroy(g.comm);
+    if (g.d_gather) (void)hipFree(g.d_gather);
+    if (g.d_frame) (void)hipFree(g.d_frame);
+    if (g.ev_gather) (void)hipEventDestroy(g.ev_gather);
+    if (g.ev_gather_start) (void)hipEventDestroy(g.ev_gather_start);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = RendererState{};
     return VCRT_SUCCESS;
 }
 
+vcrt_result vcrt_comm_unique_id(vcrt_comm_id* id) {
+    static_assert(sizeof(vcrt_comm_id) == sizeof(ncclUniqueId), "vcrt_comm_id is an ncclUniqueId");
+    if (!id) return VCRT_ERROR_INITIALIZATION_FAILED;
+    ncclUniqueId u;
+    const VkResult r = nccl_vk(ncclGetUniqueId(&u));
+    if (r != VK_SUCCESS) return r;
+    std::memcpy(id->internal, u.internal, sizeof(u.internal));
+    return VCRT_SUCCESS;
+}
+
+vcrt_result vcrt_comm_init(const vcrt_comm_id* id) {
+    if (!g.begun || !id) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (g.comm) return VCRT_ERROR_INITIALIZATION_FAILED;  // once per vcrt_begin
+    VCRT_TRY(hipSetDevice(g.device));  // RCCL binds the communicator to the current device
+    VCRT_TRY(hipStreamSynchronize(g.stream));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id->internal, sizeof(u.internal));
+    VkResult r = nccl_vk(ncclCommInitRank(&g.comm, g.desc.world_size, u, g.desc.rank));
+    if (r != VK_SUCCESS) {
+        g.comm = nullptr;
+        return r;
+    }
+    VCRT_TRY(hipEventCreate(&g.ev_gather_start));
+    VCRT_TRY(hipEventCreate(&g.ev_gather));
+    if (g.desc.world_size > 1 && g.desc.rank == 0) {
+        const size_t slab = static_cast<size_t>(g.pad_tiles) * 64 * sizeof(float4);
+        VCRT_TRY(hipMalloc(&g.d_gather, slab * static_cast<size_t>(g.desc.world_size)));
+        VCRT_TRY(hipMemset(g.d_gather, 0, slab * static_cast<size_t>(g.desc.world_size)));
+        const size_t frame = static_cast<size_t>(g.desc.width) * g.desc.height * sizeof(float4);
+        VCRT_TRY(hipMalloc(&g.d_frame, frame));
+        VCRT_TRY(hipMemset(g.d_frame, 0, frame));
+        g.d_fb = g.d_gather;  // rank 0 renders straight into its slot of the gather buffer
+    } else {
+        g.d_fb = g.d_fb_own;
+    }
+    return VCRT_SUCCESS;
+}
+
 vcrt_result vcrt_local_layout(uint32_t* elements, uint32_t* tiles) {
     if (!g.begun || !elements || !tiles) return VCRT_ERROR_INITIALIZATION_FAILED;
-    *elements = g.local_elems;
+    *elements = fb_view().elems;
     *tiles = g.local_tiles;
     return VCRT_SUCCESS;
 }
 
 vcrt_result vcrt_read_framebuffer(float* rgba, size_t count) {
-    if (!g.begun || (!rgba && g.fb_bytes)) return VCRT_ERROR_INITIALIZATION_FAILED;
-    if (count * sizeof(float) < g.fb_bytes) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
-    if (g.fb_bytes) VCRT_TRY(hipMemcpy(rgba, g.d_fb, g.fb_bytes, hipMemcpyDeviceToHost));
+    const FbView v = fb_view();
+    const size_t bytes = static_cast<size_t>(v.elems) * sizeof(float4);
+    if (!g.begun || (!rgba && bytes)) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (count * sizeof(float) < bytes) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
+    if (bytes) VCRT_TRY(hipMemcpy(rgba, v.ptr, bytes, hipMemcpyDeviceToHost));
     return VCRT_SUCCESS;
 }
 
 vcrt_result vcrt_framebuffer_device(void** device_ptr, size_t* bytes) {
     if (!g.begun || !device_ptr || !bytes) return VCRT_ERROR_INITIALIZATION_FAILED;
-    *device_ptr = g.d_fb;
-    *bytes = g.fb_bytes;
+    const FbView v = fb_view();
+    *device_ptr = v.ptr;
+    *bytes = static_cast<size_t>(v.elems) * sizeof(float4);
     return VCRT_SUCCESS;
 }
 
 vcrt_result vcrt_set_framebuffer_device(void* device_ptr, size_t bytes) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (g.comm) return VCRT_ERROR_FEATURE_NOT_PRESENT;  // the gather owns the buffers
     if (device_ptr == nullptr) {
         g.d_fb = g.d_fb_own;
         return VCRT_SUCCESS;
@@ -879,15 +1001,18 @@ vcrt_result vcrt_selftest_sin(uint32_t first, uint32_t count, uint64_t* mismatch
 }
 
 vcrt_result vcrt_read_framebuffer_srgb8(uint8_t* rgba8, size_t bytes) {
-    if (!g.begun || (!rgba8 && g.local_elems)) return VCRT_ERROR_INITIALIZATION_FAILED;
-    if (bytes < static_cast<size_t>(g.local_elems) * 4) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
-    if (!g.local_elems) return VCRT_SUCCESS;
-    if (!g.d_srgb) VCRT_TRY(hipMalloc(&g.d_srgb, sizeof(uchar4) * g.local_elems));
-    vcrt::EncodeParams ep{g.d_fb, g.d_srgb, g.d_srgb_thresholds, g.local_elems};
-    const uint32_t grid = std::min<uint32_t>((g.local_elems + 255) / 256, 4096);
+    const FbView v = fb_view();
+    if (!g.begun || (!rgba8 && v.elems)) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (bytes < static_cast<size_t>(v.elems) * 4) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
+    if (!v.elems) return VCRT_SUCCESS;
+    if (g.d_srgb) (void)hipFree(g.d_srgb);  // the view may have grown (vcrt_comm_init)
+    g.d_srgb = nullptr;
+    VCRT_TRY(hipMalloc(&g.d_srgb, sizeof(uchar4) * v.elems));
+    vcrt::EncodeParams ep{v.ptr, g.d_srgb, g.d_srgb_thresholds, v.elems};
+    const uint32_t grid = std::min<uint32_t>((v.elems + 255) / 256, 4096);
     VkResult r = launch(g.k_encode, grid, 256, 0, ep);
     if (r != VK_SUCCESS) return r;
-    VCRT_TRY(hipMemcpyAsync(rgba8, g.d_srgb, sizeof(uchar4) * g.local_elems,
+    VCRT_TRY(hipMemcpyAsync(rgba8, g.d_srgb, sizeof(uchar4) * v.elems,
                             hipMemcpyDeviceToHost, g.stream));
     VCRT_TRY(hipStreamSynchronize(g.stream));
     return VCRT_SUCCESS;

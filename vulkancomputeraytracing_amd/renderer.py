@@ -164,18 +164,36 @@ class Renderer:
     def draw_next_frame(self) -> None:
         N.check("vcrt_draw_next_frame", self._lib.vcrt_draw_next_frame())
 
+    def comm_init(self, comm_id: bytes) -> None:
+        """Join the multi-GPU frame gather (vcrt_comm_init, RCCL inside libvcrt): every rank
+        passes the same id (comm_unique_id() of rank 0). Afterwards draw_next_frame on rank 0
+        returns the whole frame, which read_framebuffer gives as [height, width, 4]."""
+        raw = bytes(comm_id)
+        if len(raw) != ctypes.sizeof(N.vcrt_comm_id):
+            raise ValueError("a comm id is 128 bytes (vcrt_comm_unique_id)")
+        cid = N.vcrt_comm_id()
+        ctypes.memmove(ctypes.addressof(cid), raw, len(raw))  # c_char arrays stop at NUL
+        N.check("vcrt_comm_init", self._lib.vcrt_comm_init(ctypes.byref(cid)))
+        self._gathering = True
+
     def local_layout(self) -> tuple[int, int]:
         """(float4 elements, tiles) of the rank-local framebuffer."""
         e, t = ctypes.c_uint32(), ctypes.c_uint32()
         N.check("vcrt_local_layout", self._lib.vcrt_local_layout(ctypes.byref(e), ctypes.byref(t)))
         return e.value, t.value
 
-    def read_framebuffer(self) -> np.ndarray:
-        """Rank-local framebuffer, float32 rgba: world 1 -> [height, width, 4] (top row first);
-        world > 1 -> packed tiles [tiles, 64, 4] (element 8*(y%8) + x%8)."""
+    def _frame_shape(self) -> tuple[int, ...]:
         elems, tiles = self.local_layout()
-        shape = ((self.desc.height, self.desc.width, 4) if self.desc.world_size == 1
-                 else (tiles, 64, 4))
+        if elems == self.desc.width * self.desc.height and (
+                self.desc.world_size == 1 or getattr(self, "_gathering", False)):
+            return (self.desc.height, self.desc.width, 4)
+        return (tiles, 64, 4)
+
+    def read_framebuffer(self) -> np.ndarray:
+        """Framebuffer, float32 rgba: the frame [height, width, 4] (top row first) at world 1 and
+        on rank 0 after comm_init; otherwise the rank's packed tiles [tiles, 64, 4] (element
+        8*(y%8) + x%8)."""
+        shape = self._frame_shape()
         out = np.empty(shape, dtype=np.float32)
         N.check("vcrt_read_framebuffer", self._lib.vcrt_read_framebuffer(
             out.ctypes.data_as(ctypes.c_void_p), out.size))
@@ -184,9 +202,7 @@ class Renderer:
     def read_framebuffer_srgb8(self) -> np.ndarray:
         """The rank-local framebuffer as sRGB8 RGBA (what the reference's B8G8R8A8_SRGB
         swapchain shows), uint8 with the read_framebuffer shape."""
-        elems, tiles = self.local_layout()
-        shape = ((self.desc.height, self.desc.width, 4) if self.desc.world_size == 1
-                 else (tiles, 64, 4))
+        shape = self._frame_shape()
         out = np.empty(shape, dtype=np.uint8)
         N.check("vcrt_read_framebuffer_srgb8", self._lib.vcrt_read_framebuffer_srgb8(
             out.ctypes.data_as(ctypes.c_void_p), out.size))
@@ -220,6 +236,13 @@ class Renderer:
         out = {name: getattr(s, name) for name, _ in N.vcrt_stats._fields_}
         out["debug"] = list(s.debug)
         return out
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL communicator id (vcrt_comm_unique_id) for rank 0 to hand to every rank."""
+    cid = N.vcrt_comm_id()
+    N.check("vcrt_comm_unique_id", N.lib().vcrt_comm_unique_id(ctypes.byref(cid)))
+    return ctypes.string_at(ctypes.addressof(cid), ctypes.sizeof(cid))
 
 
 def render(desc: RenderDesc, scene="final", frames: int = 1) -> tuple[np.ndarray, dict]:
