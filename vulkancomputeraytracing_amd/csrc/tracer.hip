@@ -1281,21 +1281,39 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                                             bst);
                     const uint32_t cnt = inf & 15u;
                     const uint16_t* ids = p.prim_ids + (inf >> 4);
-                    for (uint32_t k = 0; k < cnt; ++k) {  // the listed groups (tables in LDS
-                        ++iters;                          // or global memory)
+                    // the listed groups (tables in LDS or global memory): the exact test of the
+                    // four members, whose may-hit bits are collected (bit 4k + s)...
+                    uint32_t cbits = 0u;
+                    for (uint32_t k = 0; k < cnt; ++k) {
+                        ++iters;
                         const float4* g = tgroup + 5u * ids[k];
-                        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3], idf = g[4];
+                        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
                         v2f hb01, cc01, d01, hb23, cc23, d23;
                         pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
                         pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
-                        if (may_hit(hb01.x, cc01.x, d01.x))
-                            consider(candidate_t(hb01.x, d01.x, aa), __float_as_int(idf.x), mt, bst);
-                        if (may_hit(hb01.y, cc01.y, d01.y))
-                            consider(candidate_t(hb01.y, d01.y, aa), __float_as_int(idf.y), mt, bst);
-                        if (may_hit(hb23.x, cc23.x, d23.x))
-                            consider(candidate_t(hb23.x, d23.x, aa), __float_as_int(idf.z), mt, bst);
-                        if (may_hit(hb23.y, cc23.y, d23.y))
-                            consider(candidate_t(hb23.y, d23.y, aa), __float_as_int(idf.w), mt, bst);
+                        uint32_t hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
+                        hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
+                        hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
+                        hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
+                        cbits |= hits << (4u * k);
+                    }
+                    // ...then the candidates' roots, one per lane and loop trip (the wave runs
+                    // as many trips as its busiest lane has candidates, mostly one), with the
+                    // member's hb, cc and disc recomputed by the packed test's operations
+                    while (cbits) {
+                        const uint32_t b = (uint32_t)__builtin_ctz(cbits);
+                        cbits &= cbits - 1u;
+                        const uint32_t sm = b & 3u;
+                        const float4* g = tgroup + 5u * ids[b >> 2];
+                        const float4 xy = g[(sm >> 1) * 2], zr = g[(sm >> 1) * 2 + 1], idf = g[4];
+                        const bool hi = (sm & 1u) != 0;
+                        const float ocx = o.x - (hi ? xy.y : xy.x), ocy = o.y - (hi ? xy.w : xy.z);
+                        const float ocz = o.z - (hi ? zr.y : zr.x), r2 = hi ? zr.w : zr.z;
+                        const float hb = ocx * d.x + ocy * d.y + ocz * d.z;
+                        const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
+                        const float disc = hb * hb - aa * cc;
+                        const float ix = sm == 0 ? idf.x : sm == 1 ? idf.y : sm == 2 ? idf.z : idf.w;
+                        consider(candidate_t(hb, disc, aa), __float_as_int(ix), mt, bst);
                     }
                 }
                 // issued work: the big list and the loop's passes, per wave
