@@ -179,9 +179,10 @@ def validate(args, got, st, device, world):
     out["bitwise_vs_oracle"] = bool(np.array_equal(got[rows].view(np.uint32),
                                                    want.view(np.uint32)))
     if world > 1:
+        # the same accumulation chunk as the ranks used: then the frames are equal bit for bit
         ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
                                  max_depth=args.depth, device=device, kernel_variant=args.variant,
-                                 accumulate_chunk=args.chunk)
+                                 accumulate_chunk=st["accumulate_chunk"])
         with vc.Renderer(ref_desc, args.scene) as ref:
             ref.draw_next_frame()
             one = ref.read_framebuffer()
@@ -359,6 +360,7 @@ def main():
                              ref_flops / (PEAK_FP32_TFLOPS * 1e12) / (k_ms * 1e-3), 3),
                          "valu_issue_frac": prof.get("valu_issue_frac"),
                          "valu_lane_util": prof.get("valu_lane_util"),
+                         "effective_clock_ghz": prof.get("effective_clock_ghz"),
                          "profile": prof.get("source")},
             "gather_ms": round(sum(gather_ms) / len(gather_ms), 3),
         }

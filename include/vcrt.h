@@ -93,14 +93,15 @@ typedef struct vcrt_render_desc {
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
     int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 4 while the
-                                 whole frame has < 2^24 items, at least spp / 512; a function
-                                 of width, height and spp only: vcrt_work_chunk). A pixel's
-                                 samples are summed in fp32 in order within a chunk; one chunk
-                                 (>= samples_per_pixel) is divided in fp32, the reference's
-                                 sequential sum (shader.comp:46-56) exactly; several chunk sums
-                                 are quantized to 2^-32 and added exactly, so the image does not
-                                 depend on the schedule or the world size. At most 512 chunks
-                                 per pixel (progressive frames included). */
+                                 largest rank's share has < 2^23 items, at least spp / 512:
+                                 vcrt_work_chunk). A pixel's samples are summed in fp32 in order
+                                 within a chunk; one chunk (>= samples_per_pixel) is divided in
+                                 fp32, the reference's sequential sum (shader.comp:46-56)
+                                 exactly; several chunk sums are quantized to 2^-32 and added
+                                 exactly, so the image depends on the chunk only, not on the
+                                 schedule: a sharded frame equals a one-GPU render with the same
+                                 chunk. At most 512 chunks per pixel (progressive frames
+                                 included). */
     int32_t progressive; /* 0: every DrawNextFrame re-renders samples 0..spp-1 (the reference,
                             Linux.cpp:362-366). 1: frame f renders samples f*spp..(f+1)*spp-1 and
                             the framebuffer holds the average of all frames so far (the same
@@ -127,14 +128,16 @@ typedef struct vcrt_stats {
     uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
     uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
     uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */
-    uint64_t debug[24]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
+    uint64_t debug[32]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
                            active-lane sum, hit groups, fetches, last/first wave end time, sum
                            end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,
                            its uniform levels, node / group / candidate passes (CULL_FLAT),
                            candidate passes run, the whole wave, the big list, node pushes,
                            [17..18] shading and sky, block fetch; [19..22] flat passes:
                            entries dealt, live lanes offered, partial passes, passes; [23]
-                           the camera fast trace with its shading */
+                           the camera fast trace with its shading; [24..31] camera fast
+                           trace entries, its lanes, live lanes, listed-group loop trips and
+                           lane sum, root loop trips and lane sum; main-scan hit lanes */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

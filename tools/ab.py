@@ -19,7 +19,8 @@ import vulkancomputeraytracing_amd as vc  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("objects", nargs="+", help="code objects, or 'default' for the package's own")
+    p.add_argument("objects", nargs="+", help="code objects, or 'default' for the package's own; "
+                   "OBJ@VAR=VALUE,... sets environment variables for that object's renders")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spp", type=int, default=256)
@@ -33,9 +34,13 @@ def main():
     digest = {}
     for rnd in range(a.rounds):
         for obj in a.objects:
+            path, _, env = obj.partition("@")
+            for kv in filter(None, env.split(",")):
+                k, _, v = kv.partition("=")
+                os.environ[k] = v
             desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
                                  max_depth=a.depth, kernel_variant=a.variant, device=0,
-                                 code_object_path=None if obj == "default" else obj)
+                                 code_object_path=None if path == "default" else path)
             with vc.Renderer(desc, a.scene) as r:
                 for _ in range(a.frames):
                     r.draw_next_frame()
@@ -49,6 +54,8 @@ def main():
                                      "bound_tests": st["bound_tests"]}
                 if rnd == 0:
                     digest[obj] = hashlib.sha256(r.read_framebuffer().tobytes()).hexdigest()[:16]
+            for kv in filter(None, env.split(",")):
+                os.environ.pop(kv.partition("=")[0], None)
             print(f"round {rnd} {obj}: {best[obj]['msamples_per_s']:.0f} Msamples/s", flush=True)
     ref = digest[a.objects[0]]
     out = {o: dict(best[o], sha=digest[o], same_bits=digest[o] == ref) for o in a.objects}

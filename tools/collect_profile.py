@@ -1,10 +1,23 @@
-"""Collect a gpurun profiling batch (tools/gpu_profile.sh) into profiles/:
-kernel-trace stats of the bench command, PMC summaries, and profiles/traffic.json (HBM bytes per
-launch of the tracer kernel for the bench workload, corrected per MI355X_MICROARCH.md: FETCH_SIZE
-and WRITE_SIZE are KB; gfx950 FETCH_SIZE counts half the bytes of wide streaming reads, so it is
-doubled -- an upper bound for the tracer's narrow scalar loads)."""
-import csv
+"""Collect a gpurun profiling batch (tools/gpu_profile.sh) into profiles/<tag>_*:
+  <tag>_bench_{c4,c3,c2,c5}.json     the bench lines of the BASELINE configs
+  <tag>_bench_kernel_stats.csv       rocprofv3 --kernel-trace --stats of the c4 bench command
+  <tag>_pmc_summary.json             the PMC passes per config and kernel, and derived figures
+  traffic.json                       per workload key: the tracer kernel's HBM bytes per launch
+                                     and VALU figures, read by bench.py when its kernel matches
+
+Derived figures (MI355X_MICROARCH.md rocprofv3 sections):
+  hbm_bytes_per_launch = 2 * FETCH_SIZE + WRITE_SIZE (KB -> B; gfx950 FETCH_SIZE counts half
+                         the bytes of wide streaming reads, doubled: an upper bound here)
+  valu_issue_frac      = SQ_INSTS_VALU * 4 cycles / (1024 SIMDs * 2.4 GHz * kernel time): the
+                         fraction of the chip's VALU issue ceiling at its peak clock (a wave64
+                         fp32 or fp64 VALU instruction issues every 4 cycles per SIMD, measured:
+                         tools/microbench_valu.hip)
+  effective_clock_ghz  = GRBM_GUI_ACTIVE / 8 XCDs / kernel time
+  valu_lane_util       = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64): active lanes per
+                         VALU instruction
+"""
 import collections
+import csv
 import json
 import os
 import shutil
@@ -12,9 +25,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 src = os.path.join(ROOT, "gpurun_out", "prof")
-tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
+
+CFG_KEYS = {  # render_once arguments of the PMC passes (tools/gpu_profile.sh)
+    "c4": ("final", 1920, 1080, 1024, 10),
+    "c2": ("three", 800, 450, 64, 8),
+    "c5": ("stress4096", 3840, 2160, 4096, 50),
+}
 
 
 def pmc(name):
@@ -25,46 +44,72 @@ def pmc(name):
         k = r["Kernel_Name"].split("(")[0]
         agg[(k, r["Counter_Name"])] += float(r["Counter_Value"])
         calls[(k, r["Counter_Name"])] += 1
-    return {f"{k}|{c}": {"sum": v, "dispatches": calls[(k, c)]} for (k, c), v in agg.items()}
+    return {f"{k}|{c}": v / calls[(k, c)] for (k, c), v in agg.items()}  # per dispatch
 
 
+def run_stats(name):
+    """The render_once JSON (profiled run) printed into the pass's log."""
+    for line in open(os.path.join(src, name + ".log")):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise ValueError(name)
+
+
+def kernel_name(st):
+    names = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull",
+             4: "vcrt_trace_cull_lane", 5: "vcrt_trace_cull_flat"}
+    k = names[st["kernel_variant"]]
+    if st["kernel_variant"] == 4 and st["tables_in_lds"]:
+        k += "_lds_wide" if st["block_threads"] == 1024 else "_lds"
+    if st["kernel_variant"] == 5 and not st["tables_in_lds"]:
+        k += "_global"
+    return k
+
+
+for cfg in ("c4", "c3", "c2", "c5"):
+    for ext in ("json", "err"):
+        p = os.path.join(src, f"bench_{cfg}.{ext}")
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, f"{tag}_bench_{cfg}.{ext}"))
 shutil.copy(os.path.join(src, "kt", "bench_kernel_stats.csv"),
             os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
-bench = json.load(open(os.path.join(src, "kt_bench.json")))
-summary = {"bench_under_rocprof": {k: bench[k] for k in ("value", "ms_per_step", "roofline")}}
-for name in ("pmc_fetch", "pmc_write", "pmc_sq1", "pmc_sq2"):
-    if os.path.exists(os.path.join(src, name)):
-        summary[name] = pmc(name)
-with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
-    json.dump(summary, f, indent=1)
 
-kernel = bench["roofline"]["kernel"]
-fetch = summary["pmc_fetch"][f"{kernel}|FETCH_SIZE"]
-write = summary["pmc_write"][f"{kernel}|WRITE_SIZE"]
-per_launch = (2 * fetch["sum"] / fetch["dispatches"] + write["sum"] / write["dispatches"]) * 1024
-cfg = bench["config"]
-key = f"{cfg['scene']}_{cfg['width']}x{cfg['height']}_s{cfg['spp']}_d{cfg['max_depth']}_n1"
+summary = {}
 traffic_path = os.path.join(dst, "traffic.json")
 traffic = json.load(open(traffic_path)) if os.path.exists(traffic_path) else {}
-traffic[key] = {"hbm_bytes_per_launch": per_launch, "kernel": kernel, "fetch_kb": fetch["sum"] / fetch["dispatches"],
-                "write_kb": write["sum"] / write["dispatches"], "round": tag,
-                "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of tools/render_once.py "
-                        "at the bench config; FETCH_SIZE doubled (gfx950 correction)"}
-# VALUBusy / VALUUtilization (rocprofiler-sdk counter_defs.yaml, gfx950 rows):
-#   100 * SQ_ACTIVE_INST_VALU / CU_NUM / max(GRBM_GUI_ACTIVE), max over the 8 XCDs = sum / 8
-#   100 * SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64)
-sq1, sq2 = summary.get("pmc_sq1", {}), summary.get("pmc_sq2", {})
-try:
-    valu = sq2[f"{kernel}|SQ_ACTIVE_INST_VALU"]["sum"]
-    thread = sq2[f"{kernel}|SQ_THREAD_CYCLES_VALU"]["sum"]
-    gui = sq1[f"{kernel}|GRBM_GUI_ACTIVE"]["sum"] / 8
-    traffic[key]["valu_busy_pct"] = round(100 * valu / 256 / gui, 1)
-    traffic[key]["valu_utilization_pct"] = round(100 * thread / (valu * 64), 1)
-    traffic[key]["valu_note"] = ("VALUBusy = 100 SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8 "
-                                 "XCDs); VALUUtilization = 100 SQ_THREAD_CYCLES_VALU / "
-                                 "(SQ_ACTIVE_INST_VALU x 64): active lanes per VALU instruction")
-except KeyError:
-    pass
+for cfg, (scene, w, h, spp, depth) in CFG_KEYS.items():
+    if not os.path.exists(os.path.join(src, f"{cfg}_sq1")):
+        continue
+    passes = {}
+    for p in ("fetch", "write", "sq1", "sq2"):
+        passes.update(pmc(f"{cfg}_{p}"))
+    st = run_stats(f"{cfg}_sq1")
+    kernel = kernel_name(st)
+    t = st["kernel_ms"] * 1e-3
+    c = {k.split("|")[1]: v for k, v in passes.items() if k.startswith(kernel + "|")}
+    derived = {
+        "kernel": kernel,
+        "kernel_ms_profiled": st["kernel_ms"],
+        "hbm_bytes_per_launch": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024,
+        "fetch_kb": c["FETCH_SIZE"], "write_kb": c["WRITE_SIZE"],
+        "valu_issue_frac": round(c["SQ_INSTS_VALU"] * 4 / (1024 * 2.4e9 * t), 4),
+        "effective_clock_ghz": round(c["GRBM_GUI_ACTIVE"] / 8 / t / 1e9, 3),
+        "valu_lane_util": round(c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64), 4),
+        "salu_per_valu": round(c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"], 4),
+        "segments": st["segments"],
+        "valu_instr_per_segment_wave": round(c["SQ_INSTS_VALU"] * 64 / st["segments"], 1),
+    }
+    summary[cfg] = {"render": {k: st[k] for k in ("kernel_ms", "segments", "group_tests",
+                                                    "bound_tests", "kernel_variant",
+                                                    "tables_in_lds", "block_threads",
+                                                    "grid_blocks", "accumulate_chunk")},
+                    "counters_per_dispatch": passes, "derived": derived}
+    key = f"{scene}_{w}x{h}_s{spp}_d{depth}_n1"
+    traffic[key] = dict(derived, source=f"profiles/{tag}_pmc_summary.json [{cfg}]",
+                        round=tag)
+with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
+    json.dump(summary, f, indent=1)
 with open(traffic_path, "w") as f:
     json.dump(traffic, f, indent=1)
-print(json.dumps(traffic[key]))
+for cfg, s in summary.items():
+    print(cfg, json.dumps(s["derived"]))

@@ -18,6 +18,13 @@ for name, k in (("scan", 8), ("big list", 15), ("levels", 9), ("node pushes", 16
 print("cand passes per wave-iter %.2f; node %.2f group %.2f (from counters)" % (
     d[13] / wi, (st["bound_tests"] / wi), st["group_tests"] / wi))
 print("total ticks per wave-iter %.1f" % (tot / wi))
+if len(d) > 31 and d[24]:
+    print("camera trace: entries per wave-iter %.2f, camera lanes %.1f of %.1f live; listed loop "
+          "%.2f trips for %.2f groups per camera lane (util %.2f); root loop %.2f trips for %.2f "
+          "candidates per camera lane (util %.2f)" % (
+              d[24] / wi, d[25] / d[24], d[26] / d[24], d[27] / d[24], d[28] / d[25],
+              d[28] / max(1, d[27] * 64), d[29] / d[24], d[30] / d[25], d[30] / max(1, d[29] * 64)))
+    print("live lanes per wave-iter %.1f; main-scan hit lanes per wave-iter %.1f" % (d[1] / wi, d[31] / wi))
 if len(d) > 22 and d[22]:
     print("flat passes per wave-iter %.2f, partial %.2f; entries per live lane %.3f" % (
         d[22] / wi, d[21] / wi, d[19] / d[20]))

@@ -100,7 +100,7 @@ class vcrt_stats(ctypes.Structure):
         ("accumulated_spp", ctypes.c_uint64),
         ("group_tests", ctypes.c_uint64),
         ("bound_tests", ctypes.c_uint64),
-        ("debug", ctypes.c_uint64 * 24),
+        ("debug", ctypes.c_uint64 * 32),
     ]
 
 

@@ -115,25 +115,44 @@ RendererState g;
     } while (0)
 
 // Samples per work item when the caller leaves it to us: 64, halved (down to 4) while the
-// frame would be fewer than 2^24 items, so every lane of the persistent grid (~400k lanes on
-// MI355X) still gets ~40 items and the drain at the end stays short; at least spp / 512, so
-// a pixel has at most kAccumMaxChunks chunks. A function of the frame only (its 8x8-tile
-// slots and spp), not of the rank or the world size, so a sharded frame is bit-identical to a
-// one-GPU render (vcrt_math.h "Accumulation").
-int32_t default_chunk(uint64_t frame_slots, int32_t spp) {
+// largest rank's share of the frame would be fewer than 2^23 items, so every lane of the
+// persistent grid (~330k lanes on MI355X) still gets ~25 items and the drain at the end of the
+// queue stays short; at least spp / 512 (at most kAccumMaxChunks chunks per pixel). Measured at
+// the C4 workload with chunk-minor blocks: one GPU 159.9 / 151.9 / 148.8 / ~147
+// ms at K = 8 / 16 / 32 / 64; the 8-way shards 20.6 / 20.4 / 21.9 ms at K = 8 / 16 / 32. All
+// ranks of a frame use the same K (the largest rank's share decides), so a sharded frame equals
+// a one-GPU render with that K bit for bit.
+int32_t default_chunk(uint64_t rank_slots, int32_t spp) {
     int32_t k = kDefaultChunk;
-    while (k > 4 && frame_slots * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 24))
+    while (k > 4 && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 23))
         k /= 2;
     const int32_t k_min = (spp + vcrt::kAccumMaxChunks - 1) / vcrt::kAccumMaxChunks;
     return std::max(k, k_min);
 }
 
-// Samples per work item for a desc: its accumulate_chunk (capped at spp), else the default.
+// 8x8 tiles of a W x H frame owned by `rank`: (tx, ty) with (tx + ty) % world == rank
+// (vcrt_math.h tile_of / owner_of).
+uint32_t tiles_for_rank(int32_t width, int32_t height, int32_t world, int32_t rank) {
+    const uint32_t tiles_x = static_cast<uint32_t>((width + 7) / 8);
+    const uint32_t tiles_y = static_cast<uint32_t>((height + 7) / 8);
+    uint64_t n = 0;
+    for (uint32_t ty = 0; ty < tiles_y; ty++)
+        n += vcrt::tiles_in_row((static_cast<uint32_t>(rank) + static_cast<uint32_t>(world) -
+                                 ty % static_cast<uint32_t>(world)) %
+                                    static_cast<uint32_t>(world),
+                                tiles_x, static_cast<uint32_t>(world));
+    return static_cast<uint32_t>(n);
+}
+
+// Samples per work item for a desc: its accumulate_chunk (capped at spp), else the default for
+// the largest rank's share of the frame.
 int32_t work_chunk(const vcrt_render_desc& d) {
-    const uint64_t frame_slots = 64ull * static_cast<uint64_t>((d.width + 7) / 8) *
-                                 static_cast<uint64_t>((d.height + 7) / 8);
-    const int32_t k = d.accumulate_chunk > 0 ? d.accumulate_chunk
-                                             : default_chunk(frame_slots, d.samples_per_pixel);
+    uint32_t max_tiles = 0;
+    for (int32_t rr = 0; rr < d.world_size; rr++)
+        max_tiles = std::max(max_tiles, tiles_for_rank(d.width, d.height, d.world_size, rr));
+    const int32_t k = d.accumulate_chunk > 0
+                          ? d.accumulate_chunk
+                          : default_chunk(64ull * max_tiles, d.samples_per_pixel);
     return std::min(k, d.samples_per_pixel);
 }
 
@@ -157,20 +176,6 @@ void srgb_thresholds(float out[255]) {
         if (static_cast<double>(t) < lin) t = std::nextafter(t, 2.0f);
         out[k - 1] = t;
     }
-}
-
-// 8x8 tiles of a W x H frame owned by `rank`: (tx, ty) with (tx + ty) % world == rank
-// (vcrt_math.h tile_of / owner_of).
-uint32_t tiles_for_rank(int32_t width, int32_t height, int32_t world, int32_t rank) {
-    const uint32_t tiles_x = static_cast<uint32_t>((width + 7) / 8);
-    const uint32_t tiles_y = static_cast<uint32_t>((height + 7) / 8);
-    uint64_t n = 0;
-    for (uint32_t ty = 0; ty < tiles_y; ty++)
-        n += vcrt::tiles_in_row((static_cast<uint32_t>(rank) + static_cast<uint32_t>(world) -
-                                 ty % static_cast<uint32_t>(world)) %
-                                    static_cast<uint32_t>(world),
-                                tiles_x, static_cast<uint32_t>(world));
-    return static_cast<uint32_t>(n);
 }
 
 // Directory of this shared object (for the default code-object path).
@@ -512,7 +517,14 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     g.work_flags |= vcrt::kFlagReverseOrder;
     if (const char* e = std::getenv("VCRT_WORK_ORDER"))
         if (std::strcmp(e, "forward") == 0) g.work_flags &= ~vcrt::kFlagReverseOrder;
-    if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, 192))) != VK_SUCCESS) return fail(r);
+    // A block's 64 items are all the chunks of 64 / nchunks pixels (chunk-minor): the camera
+    // rays of a wave then come from a few pixels (+2.8% at the C4 workload against one chunk of
+    // a whole tile, same bits). VCRT_ITEM_ORDER=tile restores the tile-wide blocks.
+    g.work_flags |= vcrt::kFlagChunkMinor;
+    if (const char* e = std::getenv("VCRT_ITEM_ORDER"))
+        if (std::strcmp(e, "tile") == 0) g.work_flags &= ~vcrt::kFlagChunkMinor;
+    if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, sizeof(g.stats.debug)))) != VK_SUCCESS)
+        return fail(r);
 
     // The reference's world[] is compiled in; default to the same final scene.
     std::vector<vcrt_sphere> world;
@@ -745,7 +757,9 @@ vcrt_result vcrt_draw_next_frame(void) {
         } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_lds) {
             f = g.k_trace_cull_flat;
             fs = g.k_trace_cull_flat_stats;
-            lds = tab_lds_flat + 4 * vcrt::kWaveScratchBytes;
+            if (const char* e = std::getenv("VCRT_FLAT_BLOCK"))  // experiments: code objects
+                block = static_cast<uint32_t>(std::atoi(e));     // built with that block size
+            lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
         } else if (variant == VCRT_KERNEL_CULL_FLAT) {
             f = g.k_trace_cull_flat_global;
             fs = g.k_trace_cull_flat_global_stats;
@@ -777,7 +791,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (!g.direct && !g.desc.progressive)  // every frame sums from zero
             VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
         if (g.debug_stats) {
-            unsigned long long init[24] = {0, 0, 0, 0, 0, ~0ull};
+            unsigned long long init[32] = {0, 0, 0, 0, 0, ~0ull};
             VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
                                     g.stream));
         }

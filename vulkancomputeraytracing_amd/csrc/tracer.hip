@@ -717,6 +717,10 @@ struct PhaseTicks {
              push = 0, shade = 0, fetch = 0;
     uint64_t pass_entries = 0, pass_lanes = 0, partial_passes = 0, passes = 0;
     uint64_t cam = 0;  // the camera fast trace with its shading
+    // camera fast trace occupancy: entries, camera lanes, live lanes, listed-loop trips and
+    // lane sum, root-loop trips and lane sum; main shading hit lanes
+    uint64_t cam_entries = 0, cam_lanes = 0, cam_live = 0, list_trips = 0, list_sum = 0,
+             root_trips = 0, root_sum = 0, shade_hits = 0;
 };
 
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
@@ -1054,6 +1058,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     const f3 cam = mk(p.cam[9], p.cam[10], p.cam[11]);
     const uint32_t nchunks = (uint32_t)p.nchunks;
     const bool reverse = (p.flags & kFlagReverseOrder) != 0;
+    const bool chunk_minor = (p.flags & kFlagChunkMinor) != 0;
 
     bool done = false, need = true;
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
@@ -1208,12 +1213,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             const uint32_t avail = 64u - blk_next;
             const uint32_t mine = lanes_below(need_mask);
             if (need && !done && mine < avail) {
-                const uint32_t slot = blk_next + mine;
+                uint32_t slot = blk_next + mine, ch = blk_chunk;
+                if (chunk_minor) {  // item 64 j + slot of the tile = (pixel, chunk), chunk-minor
+                    const uint32_t i = 64u * blk_chunk + slot;
+                    slot = i / nchunks;
+                    ch = i - slot * nchunks;
+                }
                 const uint32_t px = 8u * blk_tx + (slot & 7u), py = 8u * blk_ty + (slot >> 3);
                 if (px < (uint32_t)p.width && py < (uint32_t)p.height) {  // edge tiles: skip
                     got = true;
                     g_lt = blk_lt;
-                    g_chunk = blk_chunk;
+                    g_chunk = ch;
                     g_slot = slot;
                     g_px = px;
                     g_py = py;
@@ -1266,7 +1276,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                                  aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(cam_now)) {
-                uint32_t iters = 0;
+                if constexpr (kStats) {
+                    ++pt.cam_entries;
+                    pt.cam_lanes += (uint64_t)__popcll(__ballot(cam_now));
+                    pt.cam_live += (uint64_t)__popcll(__ballot(1));
+                }
+                uint32_t iters = 0, roots = 0;
                 float mt = 1e5f;
                 int bst = -1;
                 if (cam_now) {
@@ -1314,7 +1329,21 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                         const float disc = hb * hb - aa * cc;
                         const float ix = sm == 0 ? idf.x : sm == 1 ? idf.y : sm == 2 ? idf.z : idf.w;
                         consider(candidate_t(hb, disc, aa), __float_as_int(ix), mt, bst);
+                        ++roots;
                     }
+                }
+                if constexpr (kStats) {
+                    uint32_t tl = iters, tr = roots, ml = iters, mr = roots;
+                    for (int off = 32; off > 0; off >>= 1) {
+                        tl += (uint32_t)__shfl_xor((int)tl, off);
+                        tr += (uint32_t)__shfl_xor((int)tr, off);
+                        mr = max(mr, (uint32_t)__shfl_xor((int)mr, off));
+                        ml = max(ml, (uint32_t)__shfl_xor((int)ml, off));
+                    }
+                    pt.list_sum += tl;
+                    pt.root_sum += tr;
+                    pt.list_trips += ml;
+                    pt.root_trips += mr;
                 }
                 // issued work: the big list and the loop's passes, per wave
                 for (int off = 32; off > 0; off >>= 1)
@@ -1368,7 +1397,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
 
         // ---- shade (textures.glsl) or sky (functions.glsl:85-89) ----
         uint64_t t_shade = 0;
-        if constexpr (kStats) t_shade = ticks();
+        if constexpr (kStats) {
+            t_shade = ticks();
+            pt.shade_hits += (uint64_t)__popcll(__ballot(best >= 0));
+        }
         fresh = shade_and_advance(max_t, best);
         if constexpr (kStats) pt.shade += ticks() - t_shade;
 
@@ -1410,6 +1442,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             atomicAdd(p.debug + 21, (unsigned long long)pt.partial_passes);
             atomicAdd(p.debug + 22, (unsigned long long)pt.passes);
             atomicAdd(p.debug + 23, (unsigned long long)pt.cam);
+            atomicAdd(p.debug + 24, (unsigned long long)pt.cam_entries);
+            atomicAdd(p.debug + 25, (unsigned long long)pt.cam_lanes);
+            atomicAdd(p.debug + 26, (unsigned long long)pt.cam_live);
+            atomicAdd(p.debug + 27, (unsigned long long)pt.list_trips);
+            atomicAdd(p.debug + 28, (unsigned long long)pt.list_sum);
+            atomicAdd(p.debug + 29, (unsigned long long)pt.root_trips);
+            atomicAdd(p.debug + 30, (unsigned long long)pt.root_sum);
+            atomicAdd(p.debug + 31, (unsigned long long)pt.shade_hits);
         }
     }
 }
@@ -1454,7 +1494,10 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats
 #ifndef VCRT_FLAT_WAVES
 #define VCRT_FLAT_WAVES 5  // waves per SIMD the flat scan is compiled for (LDS allows 5)
 #endif
-extern "C" __global__ __launch_bounds__(256)
+#ifndef VCRT_FLAT_BLOCK
+#define VCRT_FLAT_BLOCK 256  // threads per workgroup (the host's VCRT_FLAT_BLOCK must match)
+#endif
+extern "C" __global__ __launch_bounds__(VCRT_FLAT_BLOCK)
 __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, false, 4>(p, lds_tab);

@@ -65,12 +65,13 @@ struct TraceParams {
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
 };
 
-constexpr uint32_t kFlatBlockThreads = 640;  // CULL_FLAT with LDS tables: 10 waves per workgroup
 constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
 constexpr uint32_t kWaveScratchBytes = 4096;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
 constexpr uint32_t kWaveScratchBytesWide = 6400;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
+constexpr uint32_t kFlagChunkMinor = 8u;  // a block's 64 items run chunk-minor: all chunks of
+                                          // 64 / nchunks pixels (else one chunk of 64 pixels)
 constexpr uint32_t kFlagDirect = 4u;  // one work item per pixel and frame, not progressive: the
                                       // lane writes the pixel itself (no sums, no resolve pass)
 

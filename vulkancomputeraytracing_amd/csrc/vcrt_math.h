@@ -311,9 +311,9 @@ VCRT_HD float schlick(float cosine, float ior) {
 // as they are integers below 2^44 and a pixel has at most 512 chunks (< 2^53) -- and
 //     out = (float)((sum * 2^-32) / (double)spp_total).
 // Exact sums do not depend on the order of the additions, so the image is the same for any
-// schedule and any number of GPUs; it depends on K only, which defaults to a function of the
-// frame (width, height, spp). The quantized combination differs from the fp32 sequential sum
-// by less than that sum's own rounding error. A chunk sum with
+// schedule; it depends on K only (a sharded frame equals a one-GPU render with the same K).
+// The quantized combination differs from the fp32 sequential sum by less than that sum's own
+// rounding error. A chunk sum with
 // |S| >= 2^12, inf or NaN makes the pixel NaN (the reference scenes' radiance is <= 1 per
 // sample).
 constexpr float kAccumScale = 0x1p32f;
