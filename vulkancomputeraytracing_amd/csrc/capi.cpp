@@ -720,8 +720,9 @@ vcrt_result vcrt_draw_next_frame(void) {
         // sample sums in LDS (kWaveAccumBytes per wave, ahead of the tables).
         const uint32_t acc4 = 0, acc16 = 0;
         const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
+        // flat: near/far boxes (80 B per pair), 64-B group records, uint16 member indices
         const uint32_t tab_lds_flat =
-            static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 5));  // cbound_nf
+            static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 4) + 8 * g.ncgroups);
         const bool lane_lds = tab_lds + acc16 <= g.max_lds && g.cull_lane_tables != 2;
         const bool lane_wide = lane_lds && tab_lds + acc4 > 32768u;
         int variant = g.desc.kernel_variant;

@@ -568,6 +568,27 @@ struct WaveScratch {
 static_assert(sizeof(WaveScratch<false>) == kWaveScratchBytes, "host LDS size");
 static_assert(sizeof(WaveScratch<true>) == kWaveScratchBytesWide, "host LDS size");
 
+// The flat scans' hierarchy group records. Global tables (kWide): the 80-B records of
+// TraceParams.cgroup (four pair-SoA float4s + the members' world[] indices as int bits). LDS
+// tables: the four float4s (64 B per group) and the indices as uint16 in a table of their own
+// (8 B per group): 1 KB less LDS per workgroup for the final scene's 128 groups.
+template <bool kWide>
+struct GroupTab {
+    const float4* geom;
+    const uint16_t* idx;  // LDS layout only
+    __device__ __forceinline__ const float4* rec(uint32_t gi) const {
+        return geom + (kWide ? 5u : 4u) * gi;
+    }
+    __device__ __forceinline__ int index(uint32_t gi, uint32_t s) const {
+        if constexpr (kWide) {
+            const float4 idf = geom[5u * gi + 4u];
+            return __float_as_int(s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w);
+        } else {
+            return (int)idx[4u * gi + s];
+        }
+    }
+};
+
 __device__ __forceinline__ unsigned long long pack_hit(float t, int idx) {
     return ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)idx;
 }
@@ -617,7 +638,7 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 template <int kKind, bool kWide>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
                                           uint32_t rank, uint32_t lane, WaveScratch<kWide>* ws,
-                                          const float4* tbound, const float4* tgroup,
+                                          const float4* tbound, const GroupTab<kWide>& tg,
                                           const FlatRay& my) {
     using F = FlatFmt<kWide>;
     using entry_t = typename F::entry_t;
@@ -664,7 +685,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const float ox = from_lane(src, my.ox), oy = from_lane(src, my.oy), oz = from_lane(src, my.oz);
         const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
         const float a = from_lane(src, my.a);
-        const float4* g = tgroup + 5u * (e & F::kMask);
+        const float4* g = tg.rec(e & F::kMask);
         const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
         const v2f vox = {ox, ox}, voy = {oy, oy}, voz = {oz, oz};
         const v2f vdx = {dx, dx}, vdy = {dy, dy}, vdz = {dz, dz}, a2 = {a, a};
@@ -694,8 +715,9 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
         const float a = from_lane(src, my.a);
         const uint32_t s = e & 3u;
-        const float4* g = tgroup + 5u * ((e >> 2) & F::kMask);
-        const float4 xy = g[(s >> 1) * 2], zr = g[(s >> 1) * 2 + 1], idf = g[4];
+        const uint32_t gi = (e >> 2) & F::kMask;
+        const float4* g = tg.rec(gi);
+        const float4 xy = g[(s >> 1) * 2], zr = g[(s >> 1) * 2 + 1];
         const bool hi = (s & 1u) != 0;
         const float cx = hi ? xy.y : xy.x, cy = hi ? xy.w : xy.z;
         const float cz = hi ? zr.y : zr.x, r2 = hi ? zr.w : zr.z;
@@ -704,9 +726,8 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
         const float disc = hb * hb - a * cc;
         const float t = candidate_t(hb, disc, a);
-        const float ix = s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w;
         if (act && t > 0.001f && t < 1e5f)
-            atomicMin(&ws->key[e >> (F::kShift + 2)], pack_hit(t, __float_as_int(ix)));
+            atomicMin(&ws->key[e >> (F::kShift + 2)], pack_hit(t, tg.index(gi, s)));
     }
 }
 
@@ -733,7 +754,7 @@ template <bool kStats, bool kWide>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
                                            WaveScratch<kWide>* ws, FlatStacks& h,
                                            const float4* tbound,
-                                           const float4* tgroup, const FlatRay& my,
+                                           const GroupTab<kWide>& tg, const FlatRay& my,
                                            uint32_t& n_groups, uint32_t& n_bounds,
                                            PhaseTicks& pt) {
     uint32_t nc = h.cand, ng = h.group, nn = h.node;
@@ -762,18 +783,18 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         else if (nn >= nact) kind = 2;
         else if (th == 1u) kind = nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
-            flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tgroup, my);
+            flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tg, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (kind == 1) {
             ++n_groups;
-            flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tgroup, my);
+            flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tg, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
             n_bounds += 8;
-            flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tgroup, my);
+            flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else {
             break;
@@ -786,7 +807,7 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
 
 template <bool kStats, bool kWide>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
-                                                 const float4* tgroup, WaveScratch<kWide>* ws,
+                                                 const GroupTab<kWide>& tg, WaveScratch<kWide>* ws,
                                                  const f3 o, const f3 d, bool primary,
                                                  uint32_t item, float& max_t, int& best,
                                                  uint64_t& groups_tested, uint64_t& bounds_tested,
@@ -886,7 +907,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             }
             if constexpr (kStats) pt.push += ticks() - t0;
         }
-        flat_drain<kStats, kWide>(th, nact, rank, lane, ws, h, tbound, tgroup, my, n_groups,
+        flat_drain<kStats, kWide>(th, nact, rank, lane, ws, h, tbound, tg, my, n_groups,
                                   n_bounds,
                            pt);
         if (base >= ncg) break;
@@ -1040,15 +1061,34 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     // global memory and 32-bit entries (kCull 5)
     constexpr bool kWide = kCull == 5;
     WaveScratch<kWide>* ws = nullptr;
-    if constexpr (kCull == 2 || kCull == 4) {
-        const int nb = (p.ncgroups >> 1) * (kNearFar ? 5 : 4), ng = p.ncgroups * 5;
+    GroupTab<kWide> tg{tgroup, nullptr};  // the flat scans' view of the group records
+    if constexpr (kCull == 2) {
+        const int nb = (p.ncgroups >> 1) * 4, ng = p.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = tgroup[i];
         __syncthreads();
         tbound = lds_geom;
         tgroup = lds_geom + nb;
-        if constexpr (kCull == 4)
-            ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
+    }
+    if constexpr (kCull == 4) {  // LDS: near/far boxes, 64-B group records, uint16 indices
+        const int nb = (p.ncgroups >> 1) * 5, ng = p.ncgroups * 4;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
+        for (int i = threadIdx.x; i < ng; i += blockDim.x)
+            lds_geom[nb + i] = tgroup[5 * (i >> 2) + (i & 3)];
+        uint16_t* idx = reinterpret_cast<uint16_t*>(lds_geom + nb + ng);
+        for (int i = threadIdx.x; i < p.ncgroups; i += blockDim.x) {
+            const float4 idf = tgroup[5 * i + 4];  // member indices < 2^16 (<= 1024 groups)
+            idx[4 * i + 0] = (uint16_t)__float_as_int(idf.x);
+            idx[4 * i + 1] = (uint16_t)__float_as_int(idf.y);
+            idx[4 * i + 2] = (uint16_t)__float_as_int(idf.z);
+            idx[4 * i + 3] = (uint16_t)__float_as_int(idf.w);
+        }
+        __syncthreads();
+        tbound = lds_geom;
+        tg.geom = lds_geom + nb;
+        tg.idx = idx;
+        ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng + p.ncgroups / 2) +
+             (threadIdx.x >> 6);
     }
     if constexpr (kCull == 5) ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1301,7 +1341,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     uint32_t cbits = 0u;
                     for (uint32_t k = 0; k < cnt; ++k) {
                         ++iters;
-                        const float4* g = tgroup + 5u * ids[k];
+                        const float4* g = tg.rec(ids[k]);
                         const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
                         v2f hb01, cc01, d01, hb23, cc23, d23;
                         pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
@@ -1319,16 +1359,16 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                         const uint32_t b = (uint32_t)__builtin_ctz(cbits);
                         cbits &= cbits - 1u;
                         const uint32_t sm = b & 3u;
-                        const float4* g = tgroup + 5u * ids[b >> 2];
-                        const float4 xy = g[(sm >> 1) * 2], zr = g[(sm >> 1) * 2 + 1], idf = g[4];
+                        const uint32_t gi = ids[b >> 2];
+                        const float4* g = tg.rec(gi);
+                        const float4 xy = g[(sm >> 1) * 2], zr = g[(sm >> 1) * 2 + 1];
                         const bool hi = (sm & 1u) != 0;
                         const float ocx = o.x - (hi ? xy.y : xy.x), ocy = o.y - (hi ? xy.w : xy.z);
                         const float ocz = o.z - (hi ? zr.y : zr.x), r2 = hi ? zr.w : zr.z;
                         const float hb = ocx * d.x + ocy * d.y + ocz * d.z;
                         const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
                         const float disc = hb * hb - aa * cc;
-                        const float ix = sm == 0 ? idf.x : sm == 1 ? idf.y : sm == 2 ? idf.z : idf.w;
-                        consider(candidate_t(hb, disc, aa), __float_as_int(ix), mt, bst);
+                        consider(candidate_t(hb, disc, aa), tg.index(gi, sm), mt, bst);
                         ++roots;
                     }
                 }
@@ -1374,7 +1414,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kCull == 4 || kCull == 5)
-                    scan_culled_flat<kStats, kWide>(p, tbound, tgroup, ws, o, d, pass == 0, q,
+                    scan_culled_flat<kStats, kWide>(p, tbound, tg, ws, o, d, pass == 0, q,
                                                     max_t, best, w_groups, w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
