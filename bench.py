@@ -25,8 +25,6 @@ PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector (packed FMA), MI355X_MICROA
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
 FLOPS_PER_BOUND_TEST = 26       # tracer.hip box_gap, per box: 6 fma 12, per-axis min/max 6,
                                 # tnear/tfar 4, gap sub + add + fma 4
-KERNEL_NAMES = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull",
-                4: "vcrt_trace_cull_lane", 5: "vcrt_trace_cull_flat"}
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -285,11 +283,7 @@ def main():
         value = samples / elapsed / 1e6
         k_ms = sum(kernel_ms) / len(kernel_ms)
         seg = sum(segments) / len(segments)
-        kernel = KERNEL_NAMES.get(st["kernel_variant"], "?")
-        if st["kernel_variant"] == 4 and st["tables_in_lds"]:
-            kernel += "_lds_wide" if st["block_threads"] == 1024 else "_lds"
-        if st["kernel_variant"] == 5 and not st["tables_in_lds"]:
-            kernel += "_global"
+        kernel = st["kernel"]  # the symbol the timed frames launched (vcrt_stats.kernel)
         # Issued work of the timed kernel (the roofline numerator): every lane of each
         # wave-level exact group test (4 spheres x 23 flops, functions.glsl:15-19) and box test
         # (26 flops), counted by in-kernel per-wave counters; the linear scans issue the

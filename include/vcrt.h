@@ -128,6 +128,7 @@ typedef struct vcrt_stats {
     uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
     uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
     uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */
+    char kernel[48];       /* the tracer kernel the last frame launched (its code-object symbol) */
     uint64_t debug[32]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
                            active-lane sum, hit groups, fetches, last/first wave end time, sum
                            end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,

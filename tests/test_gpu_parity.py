@@ -550,3 +550,18 @@ def test_camera_ray_lists_switch_keeps_bits(monkeypatch):
     assert_bitwise(outs[0][0], outs[1][0], "lists off vs on")
     assert outs[0][1]["segments"] == outs[1][1]["segments"]
     assert outs[0][1]["bound_tests"] > outs[1][1]["bound_tests"]  # the lists skipped box tests
+
+
+@pytest.mark.parametrize("scene,variant,kernel", [
+    ("final", vc.KERNEL_AUTO, "vcrt_trace_cull_flat"),
+    ("three", vc.KERNEL_AUTO, "vcrt_trace_smem"),
+    ("stress4096", vc.KERNEL_AUTO, "vcrt_trace_cull_flat_global"),
+    ("final", vc.KERNEL_LDS, "vcrt_trace_lds"),
+    ("final", vc.KERNEL_CULL, "vcrt_trace_cull"),
+    ("final", vc.KERNEL_CULL_LANE, "vcrt_trace_cull_lane_lds"),
+])
+def test_stats_name_the_launched_kernel(scene, variant, kernel):
+    """vcrt_stats.kernel (and the shader stage's pName, Shader.cpp:89's analogue) is the code-
+    object symbol the frame dispatched: what bench.py reports and rocprof lists."""
+    _, st = gpu_render(scene, 64, 36, 1, 4, variant)
+    assert st["kernel"] == kernel

@@ -56,14 +56,7 @@ def run_stats(name):
 
 
 def kernel_name(st):
-    names = {1: "vcrt_trace_lds", 2: "vcrt_trace_smem", 3: "vcrt_trace_cull",
-             4: "vcrt_trace_cull_lane", 5: "vcrt_trace_cull_flat"}
-    k = names[st["kernel_variant"]]
-    if st["kernel_variant"] == 4 and st["tables_in_lds"]:
-        k += "_lds_wide" if st["block_threads"] == 1024 else "_lds"
-    if st["kernel_variant"] == 5 and not st["tables_in_lds"]:
-        k += "_global"
-    return k
+    return st["kernel"]  # vcrt_stats.kernel: the symbol the profiled frame launched
 
 
 for cfg in ("c4", "c3", "c2", "c5"):

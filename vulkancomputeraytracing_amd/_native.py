@@ -100,6 +100,7 @@ class vcrt_stats(ctypes.Structure):
         ("accumulated_spp", ctypes.c_uint64),
         ("group_tests", ctypes.c_uint64),
         ("bound_tests", ctypes.c_uint64),
+        ("kernel", ctypes.c_char * 48),
         ("debug", ctypes.c_uint64 * 32),
     ]
 

@@ -746,39 +746,51 @@ vcrt_result vcrt_draw_next_frame(void) {
         const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
                               g.ncgroups <= vcrt::kFlatMaxGroups;
         hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
+        const char* fname = "vcrt_trace_smem";
         uint32_t block = 256;
         uint32_t lds = acc4;
         if (variant == VCRT_KERNEL_LDS) {
             f = g.k_trace_lds;
             fs = g.k_trace_lds_stats;
+            fname = "vcrt_trace_lds";
             lds = acc4 + geom_lds;
         } else if (variant == VCRT_KERNEL_CULL) {
             f = g.k_trace_cull;
             fs = g.k_trace_cull_stats;
+            fname = "vcrt_trace_cull";
         } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_lds) {
             f = g.k_trace_cull_flat;
             fs = g.k_trace_cull_flat_stats;
+            fname = "vcrt_trace_cull_flat";
             if (const char* e = std::getenv("VCRT_FLAT_BLOCK"))  // experiments: code objects
                 block = static_cast<uint32_t>(std::atoi(e));     // built with that block size
             lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
         } else if (variant == VCRT_KERNEL_CULL_FLAT) {
             f = g.k_trace_cull_flat_global;
             fs = g.k_trace_cull_flat_global_stats;
+            fname = "vcrt_trace_cull_flat_global";
             lds = 4 * vcrt::kWaveScratchBytesWide;
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
             f = g.k_trace_cull_lane_lds_wide;
             fs = g.k_trace_cull_lane_lds_wide_stats;
+            fname = "vcrt_trace_cull_lane_lds_wide";
             block = 1024;
             lds = acc16 + tab_lds;
         } else if (variant == VCRT_KERNEL_CULL_LANE && lane_lds) {
             f = g.k_trace_cull_lane_lds;
             fs = g.k_trace_cull_lane_lds_stats;
+            fname = "vcrt_trace_cull_lane_lds";
             lds = acc4 + tab_lds;
         } else if (variant == VCRT_KERNEL_CULL_LANE) {
             f = g.k_trace_cull_lane;
             fs = g.k_trace_cull_lane_stats;
+            fname = "vcrt_trace_cull_lane";
         }
         if (g.debug_stats) f = fs;
+        // the stage names the entry point this draw dispatches (Shader.cpp:89 names "main")
+        g.stage.pName = fname;
+        std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s%s", fname,
+                      g.debug_stats ? "_stats" : "");
         int per_cu = g.desc.blocks_per_cu;
         if (per_cu <= 0) {
             per_cu = 0;

@@ -43,7 +43,9 @@ VkResult CreateShaderStageFromFile(IN const char* filename, IN VkShaderStageFlag
     info->sType = 18;  // VK_STRUCTURE_TYPE_PIPELINE_SHADER_STAGE_CREATE_INFO
     info->stage = stage;
     info->module = module;
-    info->pName = "vcrt_trace_lds";
+    // the entry point vcrt_draw_next_frame dispatches for the reference's own scene (AUTO on
+    // the final scene); each draw then sets the stage's pName to the kernel it launched
+    info->pName = "vcrt_trace_cull_flat";
     return VK_SUCCESS;
 }
 

@@ -235,6 +235,7 @@ class Renderer:
         N.check("vcrt_get_stats", self._lib.vcrt_get_stats(ctypes.byref(s)))
         out = {name: getattr(s, name) for name, _ in N.vcrt_stats._fields_}
         out["debug"] = list(s.debug)
+        out["kernel"] = s.kernel.decode()
         return out
 
 
