@@ -169,10 +169,10 @@ def test_work_chunk_rule(w, h, spp):
         k = ks.pop()
         assert 1 <= k <= spp
         assert -(-spp // k) <= 512
-        assert k == spp or k >= 4
+        assert k == spp or k >= 16
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
         want = 64
-        while want > 4 and slots * -(-spp // want) < (1 << 23):
+        while want > 16 and slots * -(-spp // want) < (1 << 23):
             want //= 2
         assert k == min(max(want, -(-spp // 512)), spp)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,

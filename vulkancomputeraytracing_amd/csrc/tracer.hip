@@ -1204,9 +1204,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                                     acc.z == acc.z;
                     const double nan = __builtin_nan("");
                     double* s = p.accum + 4u * q;
+#ifdef VCRT_EXPERIMENT_NO_ATOMICS  // timing experiments only: wrong image
+                    if (acc.x == 12345.0f) s[0] = ok ? 1.0 : nan;
+#else
                     atomicAdd(s + 0, ok ? (double)__builtin_rintf(acc.x * kAccumScale) : nan);
                     atomicAdd(s + 1, ok ? (double)__builtin_rintf(acc.y * kAccumScale) : nan);
                     atomicAdd(s + 2, ok ? (double)__builtin_rintf(acc.z * kAccumScale) : nan);
+#endif
                 }
                 need = true;
             } else {
