@@ -764,8 +764,6 @@ vcrt_result vcrt_draw_next_frame(void) {
             f = g.k_trace_cull_flat;
             fs = g.k_trace_cull_flat_stats;
             fname = "vcrt_trace_cull_flat";
-            if (const char* e = std::getenv("VCRT_FLAT_BLOCK"))  // experiments: code objects
-                block = static_cast<uint32_t>(std::atoi(e));     // built with that block size
             lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
         } else if (variant == VCRT_KERNEL_CULL_FLAT) {
             f = g.k_trace_cull_flat_global;

@@ -1538,10 +1538,7 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats
 #ifndef VCRT_FLAT_WAVES
 #define VCRT_FLAT_WAVES 5  // waves per SIMD the flat scan is compiled for (LDS allows 5)
 #endif
-#ifndef VCRT_FLAT_BLOCK
-#define VCRT_FLAT_BLOCK 256  // threads per workgroup (the host's VCRT_FLAT_BLOCK must match)
-#endif
-extern "C" __global__ __launch_bounds__(VCRT_FLAT_BLOCK)
+extern "C" __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, false, 4>(p, lds_tab);
