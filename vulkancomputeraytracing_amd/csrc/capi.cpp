@@ -76,6 +76,7 @@ struct RendererState {
     float4* d_ctop = nullptr;
     uint32_t* d_prim_info = nullptr;  // camera-ray tile lists (primary.cpp), flat scan only
     uint16_t* d_prim_ids = nullptr;
+    float4* d_cam_oc = nullptr;  // camera-relative group records (build_camera_records)
     bool primary_lists = true;        // VCRT_PRIMARY_LISTS=0 turns them off
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
@@ -219,6 +220,8 @@ void free_scene() {
     if (g.d_ctop) (void)hipFree(g.d_ctop);
     if (g.d_prim_info) (void)hipFree(g.d_prim_info);
     if (g.d_prim_ids) (void)hipFree(g.d_prim_ids);
+    if (g.d_cam_oc) (void)hipFree(g.d_cam_oc);
+    g.d_cam_oc = nullptr;
     g.d_prim_info = nullptr;
     g.d_prim_ids = nullptr;
     g.d_cgroup = nullptr;
@@ -614,6 +617,12 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
             if (!pl.ids.empty())
                 VCRT_TRY(hipMemcpy(g.d_prim_ids, pl.ids.data(), sizeof(uint16_t) * pl.ids.size(),
                                    hipMemcpyHostToDevice));
+            // the camera fast trace's camera-relative group records
+            std::vector<float> crec;
+            vcrt::build_camera_records(ct, camera_array().data(), crec);
+            VCRT_TRY(hipMalloc(&g.d_cam_oc, sizeof(float) * crec.size()));
+            VCRT_TRY(hipMemcpy(g.d_cam_oc, crec.data(), sizeof(float) * crec.size(),
+                               hipMemcpyHostToDevice));
         }
     }
     VCRT_TRY(hipMalloc(&g.d_geom, sizeof(float) * table.size()));
@@ -694,6 +703,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.ctop = g.d_ctop;
         p.prim_info = g.d_prim_info;
         p.prim_ids = g.d_prim_ids;
+        p.cam_oc = g.d_cam_oc;
         p.ncgroups = g.ncgroups;
         p.nbig = g.ncbig;
         for (int k = 0; k < 4; k++) p.box_margin[k] = g.cmargin[k];

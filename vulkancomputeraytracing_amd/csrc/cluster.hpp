@@ -49,4 +49,11 @@ struct PrimaryLists {
 void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
                          int32_t height, int32_t rank, int32_t world, PrimaryLists& out);
 
+// Camera-relative group records for the camera fast trace: for every group of ct.geom (big
+// groups first), the members' oc = camera centre - centre and cc = |oc|^2 - r^2 in the group
+// record's pair-SoA form, (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1) per pair, evaluated in fp32
+// with the kernel's operations and order (tracer.hip pair_disc_cc), so a camera ray's hb and
+// discriminant from them carry the same bits. [nbig + ngroups][16] floats.
+void build_camera_records(const CullTables& ct, const float cam[12], std::vector<float>& out);
+
 }  // namespace vcrt

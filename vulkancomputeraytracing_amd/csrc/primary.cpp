@@ -150,4 +150,27 @@ void build_primary_lists(const CullTables& ct, const float cam[12], int32_t widt
     }
 }
 
+void build_camera_records(const CullTables& ct, const float cam[12], std::vector<float>& out) {
+    const size_t nall = static_cast<size_t>(ct.nbig + ct.ngroups);
+    out.assign(nall * 16, 0.0f);
+    const float ox = cam[9], oy = cam[10], oz = cam[11];
+    for (size_t gi = 0; gi < nall; gi++) {
+        const float* g = &ct.geom[gi * 16];
+        float* c = &out[gi * 16];
+        for (int pair = 0; pair < 2; pair++)
+            for (int e = 0; e < 2; e++) {
+                // pair-SoA: (cx0,cx1,cy0,cy1) (cz0,cz1,r0^2,r1^2) per pair of members
+                const float* q = g + 8 * pair;
+                float* w = c + 8 * pair;
+                const float ocx = ox - q[0 + e], ocy = oy - q[2 + e], ocz = oz - q[4 + e];
+                // pair_disc_cc's order: ((ocx ocx + ocy ocy) + ocz ocz) - r^2, fp32, no FMA
+                const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - q[6 + e];
+                w[0 + e] = ocx;
+                w[2 + e] = ocy;
+                w[4 + e] = ocz;
+                w[6 + e] = cc;
+            }
+    }
+}
+
 }  // namespace vcrt

@@ -213,6 +213,56 @@ __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
     return (-hb + sq) / a;
 }
 
+// candidate_t for a ray of the guarded range (a in [2^-20, 2^60], |o|, |c|, r <= 2^30, so
+// |hb| < 2^63 and disc < 2^126), with ya = recip_a(a) computed once per ray. It returns the
+// same t as candidate_t wherever that t can be accepted, and a t <= min_t wherever candidate_t's
+// is (the only other use of a root: candidate_t's choice between them):
+//  * division: hipcc's correctly rounded x / a is v_div_scale (x2), a Newton-refined v_rcp,
+//    q0 = x y, two residual corrections (the second in v_div_fmas) and v_div_fixup. v_div_scale
+//    leaves both operands alone and v_div_fmas does not rescale when x, a are normal, x / a is
+//    normal and exp(x) - exp(a) < 96, exp(x) > 23 (the ISA's V_DIV_SCALE_F32); v_div_fixup only
+//    changes special values. div_a runs that unscaled sequence: for |x| in [2^-103, 2^64) the
+//    same bits. A root that can be accepted (> min_t = 0.001 with a >= 2^-20) has |x| > 2^-30.
+//    For |x| < 2^-103 (or x = 0) both quotients are below 2^-83 in magnitude, so both roots
+//    are rejected alike (their sign or last bits never matter).
+//  * sqrt: hipcc's correctly rounded sqrt scales x < 2^-96, takes v_sqrt and picks between its
+//    neighbours by two FMA residuals, then special-cases 0 and inf; sqrt_unscaled runs the
+//    unscaled middle, the same bits for x in [2^-96, 2^126]. Lanes with disc < 2^-96 take the
+//    full sqrt (a zero discriminant, a grazing ray).
+__device__ __forceinline__ float recip_a(float a) {
+    const float y0 = __builtin_amdgcn_rcpf(a);
+    return __builtin_fmaf(__builtin_fmaf(-a, y0, 1.0f), y0, y0);
+}
+
+__device__ __forceinline__ float div_a(float x, float a, float ya) {
+    const float q0 = x * ya;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-a, q0, x), ya, q0);
+    return __builtin_fmaf(__builtin_fmaf(-a, q1, x), ya, q1);
+}
+
+__device__ __forceinline__ float sqrt_unscaled(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    return __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+}
+
+__device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a, float ya) {
+#ifdef VCRT_EXACT_CANDIDATE_OPS  // A/B builds: hipcc's full sequences
+    return candidate_t(hb, disc, a);
+#else
+    float sq = sqrt_unscaled(disc);
+    if (disc < 0x1p-96f) {
+        asm volatile("");  // a real branch: hipcc would otherwise run the full sqrt for every lane
+        sq = __builtin_sqrtf(disc);
+    }
+    const float r1 = div_a(-hb - sq, a, ya);
+    if (r1 > 0.001f) return r1;
+    return div_a(-hb + sq, a, ya);
+#endif
+}
+
 // A member whose origin lies outside or on it (cc >= 0) while the ray points away from its
 // centre (hb >= 0) can never be accepted: disc_f <= RN(hb^2) and RN(sqrt(RN(hb^2))) = hb
 // (binary fp, no underflow), so RN(-hb + sq) <= 0 and both roots are <= 0 < min_t. If hb^2
@@ -233,6 +283,18 @@ __device__ __forceinline__ void pair_disc_cc(const v2f ox, const v2f oy, const v
     const v2f ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
     hb = ocx * dx + ocy * dy + ocz * dz;
     cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
+    disc = hb * hb - a2 * cc;
+}
+
+// pair_disc_cc for a camera ray (o = the camera centre) from the camera-relative record
+// (TraceParams.cam_oc: oc and cc as pair_disc_cc computes them for that o): the remaining
+// operations, in the same order, on the same operands -- the same bits, at half the work.
+__device__ __forceinline__ void pair_disc_cam(const v2f dx, const v2f dy, const v2f dz,
+                                              const v2f a2, float4 oxy, float4 ozc, v2f& hb,
+                                              v2f& cc, v2f& disc) {
+    const v2f ocx = {oxy.x, oxy.y}, ocy = {oxy.z, oxy.w}, ocz = {ozc.x, ozc.y};
+    cc = (v2f){ozc.z, ozc.w};
+    hb = ocx * dx + ocy * dy + ocz * dz;
     disc = hb * hb - a2 * cc;
 }
 
@@ -334,8 +396,8 @@ __device__ __forceinline__ uint32_t bound_pair_need(const BoxRay& r, const Bound
 // The exact test of one group for every lane (wave-uniform scalar loads of the 80-B record):
 // the big-sphere list, tested for every ray ahead of the hierarchy.
 __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay& r, v2f dx, v2f dy,
-                                                    v2f dz, v2f a2, float a, float& max_t,
-                                                    int& best) {
+                                                    v2f dz, v2f a2, float a, float ya,
+                                                    float& max_t, int& best) {
     const float4 q0 = rec[0], q1 = rec[1], idf = rec[4];
     v2f hb01, cc01, d01, hb23 = {0.f, 0.f}, cc23 = {0.f, 0.f}, d23 = {-1.f, -1.f};
     pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
@@ -346,13 +408,36 @@ __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay&
     const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
     if (__ballot(!(m4 < 0.0f))) {
         if (may_hit(hb01.x, cc01.x, d01.x))
-            consider(candidate_t(hb01.x, d01.x, a), __float_as_int(idf.x), max_t, best);
+            consider(candidate_t_fast(hb01.x, d01.x, a, ya), __float_as_int(idf.x), max_t, best);
         if (may_hit(hb01.y, cc01.y, d01.y))
-            consider(candidate_t(hb01.y, d01.y, a), __float_as_int(idf.y), max_t, best);
+            consider(candidate_t_fast(hb01.y, d01.y, a, ya), __float_as_int(idf.y), max_t, best);
         if (may_hit(hb23.x, cc23.x, d23.x))
-            consider(candidate_t(hb23.x, d23.x, a), __float_as_int(idf.z), max_t, best);
+            consider(candidate_t_fast(hb23.x, d23.x, a, ya), __float_as_int(idf.z), max_t, best);
         if (may_hit(hb23.y, cc23.y, d23.y))
-            consider(candidate_t(hb23.y, d23.y, a), __float_as_int(idf.w), max_t, best);
+            consider(candidate_t_fast(hb23.y, d23.y, a, ya), __float_as_int(idf.w), max_t, best);
+    }
+}
+
+// exact_group_uniform for camera rays, from the group's camera-relative record `crec` (the
+// member indices still come from the group record `rec`).
+__device__ __forceinline__ void exact_group_uniform_cam(cfloat4* crec, cfloat4* rec, v2f dx,
+                                                        v2f dy, v2f dz, v2f a2, float a,
+                                                        float ya, float& max_t, int& best) {
+    const float4 c0 = crec[0], c1 = crec[1], idf = rec[4];
+    v2f hb01, cc01, d01, hb23 = {0.f, 0.f}, cc23 = {0.f, 0.f}, d23 = {-1.f, -1.f};
+    pair_disc_cam(dx, dy, dz, a2, c0, c1, hb01, cc01, d01);
+    if (__float_as_int(idf.z) >= 0 || __float_as_int(idf.w) >= 0)
+        pair_disc_cam(dx, dy, dz, a2, crec[2], crec[3], hb23, cc23, d23);
+    const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
+    if (__ballot(!(m4 < 0.0f))) {
+        if (may_hit(hb01.x, cc01.x, d01.x))
+            consider(candidate_t_fast(hb01.x, d01.x, a, ya), __float_as_int(idf.x), max_t, best);
+        if (may_hit(hb01.y, cc01.y, d01.y))
+            consider(candidate_t_fast(hb01.y, d01.y, a, ya), __float_as_int(idf.y), max_t, best);
+        if (may_hit(hb23.x, cc23.x, d23.x))
+            consider(candidate_t_fast(hb23.x, d23.x, a, ya), __float_as_int(idf.z), max_t, best);
+        if (may_hit(hb23.y, cc23.y, d23.y))
+            consider(candidate_t_fast(hb23.y, d23.y, a, ya), __float_as_int(idf.w), max_t, best);
     }
 }
 
@@ -375,7 +460,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* geom = (cfloat4*)p.cgroup;
     for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray
-        exact_group_uniform(geom + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
+        exact_group_uniform(geom + 5 * gb, r, dx, dy, dz, a2, a, recip_a(a), max_t, best);
     groups_tested += (uint64_t)p.nbig;
     geom += 5 * p.nbig;           // the hierarchy's groups
     const int ncg = p.ncgroups;  // multiple of 16: whole node pairs
@@ -621,13 +706,24 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
     return pre;
 }
 
+// Maximum over the active lanes of v < 2^kBits, wave-uniform: one compare per bit (ballots)
+// instead of a shuffle reduction.
+template <int kBits>
+__device__ __forceinline__ uint32_t wave_max_small(uint32_t v) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = kBits - 1; b >= 0; --b)
+        if (__ballot(v >= (m | (1u << b)))) m |= 1u << b;
+    return m;
+}
+
 // v of lane src_x4 / 4 (ds_bpermute; the source lane is live)
 __device__ __forceinline__ float from_lane(int src_x4, float v) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(src_x4, __float_as_int(v)));
 }
 
 struct FlatRay {  // this lane's ray, as the passes fetch it
-    float ox, oy, oz, dx, dy, dz, a;
+    float ox, oy, oz, dx, dy, dz, a, ya;
     BoxRay br;
 };
 
@@ -713,7 +809,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const int src = (int)(e >> (F::kShift + 2)) << 2;
         const float ox = from_lane(src, my.ox), oy = from_lane(src, my.oy), oz = from_lane(src, my.oz);
         const float dx = from_lane(src, my.dx), dy = from_lane(src, my.dy), dz = from_lane(src, my.dz);
-        const float a = from_lane(src, my.a);
+        const float a = from_lane(src, my.a), ya = from_lane(src, my.ya);
         const uint32_t s = e & 3u;
         const uint32_t gi = (e >> 2) & F::kMask;
         const float4* g = tg.rec(gi);
@@ -725,7 +821,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const float hb = ocx * dx + ocy * dy + ocz * dz;
         const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
         const float disc = hb * hb - a * cc;
-        const float t = candidate_t(hb, disc, a);
+        const float t = candidate_t_fast(hb, disc, a, ya);
         if (act && t > 0.001f && t < 1e5f)
             atomicMin(&ws->key[e >> (F::kShift + 2)], pack_hit(t, tg.index(gi, s)));
     }
@@ -826,6 +922,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     my.dy = d.y;
     my.dz = d.z;
     my.a = dot(d, d);
+    my.ya = recip_a(my.a);
     my.br = box_ray(p, o, d);
     const BoxRay& br = my.br;
     CullRay r;
@@ -835,7 +932,8 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     {
         const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {my.a, my.a};
         for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
-            exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, my.a, max_t, best);
+            exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, my.a, my.ya, max_t,
+                                best);
     }
     if constexpr (kStats) pt.big += ticks() - t_in;
     uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
@@ -938,7 +1036,8 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
     cfloat4* top = (cfloat4*)p.ctop;
     const int ncg = p.ncgroups;
     for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
-        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, a, max_t, best);
+        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, a, recip_a(a), max_t,
+                            best);
     // per-segment pass counters, wave-uniform: kept in SGPRs, folded into the 64-bit totals once
     uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
     uint32_t tops = 0;
@@ -1330,26 +1429,27 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 int bst = -1;
                 if (cam_now) {
                     ++segs;
-                    CullRay r;
-                    r.ox = (v2f){o.x, o.x};
-                    r.oy = (v2f){o.y, o.y};
-                    r.oz = (v2f){o.z, o.z};
+                    // A camera ray starts at the camera centre: its members' oc and cc come
+                    // from the camera-relative records (pair_disc_cam: same bits, half the
+                    // arithmetic of pair_disc_cc); the roots take candidate_t_fast.
+                    cfloat4* crec = (cfloat4*)p.cam_oc;
+                    const float ya = recip_a(aa);
                     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
                     for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres (scalar loads)
-                        exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, aa, mt,
-                                            bst);
+                        exact_group_uniform_cam(crec + 4 * gb, (cfloat4*)p.cgroup + 5 * gb, dx, dy,
+                                                dz, a2, aa, ya, mt, bst);
                     const uint32_t cnt = inf & 15u;
                     const uint16_t* ids = p.prim_ids + (inf >> 4);
-                    // the listed groups (tables in LDS or global memory): the exact test of the
-                    // four members, whose may-hit bits are collected (bit 4k + s)...
+                    // the listed groups: the exact test of the four members, whose may-hit
+                    // bits are collected (bit 4k + s)...
                     uint32_t cbits = 0u;
                     for (uint32_t k = 0; k < cnt; ++k) {
                         ++iters;
-                        const float4* g = tg.rec(ids[k]);
-                        const float4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
+                        const float4* c = p.cam_oc + 4u * ((uint32_t)p.nbig + ids[k]);
+                        const float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3];
                         v2f hb01, cc01, d01, hb23, cc23, d23;
-                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
-                        pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
+                        pair_disc_cam(dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
+                        pair_disc_cam(dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
                         uint32_t hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
                         hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
                         hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
@@ -1358,21 +1458,20 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     }
                     // ...then the candidates' roots, one per lane and loop trip (the wave runs
                     // as many trips as its busiest lane has candidates, mostly one), with the
-                    // member's hb, cc and disc recomputed by the packed test's operations
+                    // member's hb and disc recomputed by the same operations
                     while (cbits) {
                         const uint32_t b = (uint32_t)__builtin_ctz(cbits);
                         cbits &= cbits - 1u;
                         const uint32_t sm = b & 3u;
                         const uint32_t gi = ids[b >> 2];
-                        const float4* g = tg.rec(gi);
-                        const float4 xy = g[(sm >> 1) * 2], zr = g[(sm >> 1) * 2 + 1];
+                        const float4* c = p.cam_oc + 4u * ((uint32_t)p.nbig + gi);
+                        const float4 xy = c[(sm >> 1) * 2], zc = c[(sm >> 1) * 2 + 1];
                         const bool hi = (sm & 1u) != 0;
-                        const float ocx = o.x - (hi ? xy.y : xy.x), ocy = o.y - (hi ? xy.w : xy.z);
-                        const float ocz = o.z - (hi ? zr.y : zr.x), r2 = hi ? zr.w : zr.z;
+                        const float ocx = hi ? xy.y : xy.x, ocy = hi ? xy.w : xy.z;
+                        const float ocz = hi ? zc.y : zc.x, cc = hi ? zc.w : zc.z;
                         const float hb = ocx * d.x + ocy * d.y + ocz * d.z;
-                        const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
                         const float disc = hb * hb - aa * cc;
-                        consider(candidate_t(hb, disc, aa), tg.index(gi, sm), mt, bst);
+                        consider(candidate_t_fast(hb, disc, aa, ya), tg.index(gi, sm), mt, bst);
                         ++roots;
                     }
                 }
@@ -1390,9 +1489,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     pt.root_trips += mr;
                 }
                 // issued work: the big list and the loop's passes, per wave
-                for (int off = 32; off > 0; off >>= 1)
-                    iters = max(iters, (uint32_t)__shfl_xor((int)iters, off));
-                w_groups += (uint64_t)p.nbig + iters;
+                w_groups += (uint64_t)p.nbig + wave_max_small<4>(iters);
                 if (cam_now) fresh = shade_and_advance(mt, bst);
             }
             if constexpr (kStats) pt.cam += ticks() - t_cam;

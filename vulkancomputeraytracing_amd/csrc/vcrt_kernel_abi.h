@@ -49,6 +49,10 @@ struct TraceParams {
                                 //   (4 lt + 2 qy + qx) of each local tile: offset << 4 |
                                 //   count (count <= 8; 15 = none), or null
     const uint16_t* prim_ids;   // hierarchy group indices of those lists
+    const float4* cam_oc;       // [(nbig + ncgroups) * 4] with the lists: per group the members'
+                                //   oc = camera centre - centre and cc = |oc|^2 - r^2, pair-SoA
+                                //   (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1) (..2,3..), fp32 as
+                                //   pair_disc_cc computes them (cluster.hpp build_camera_records)
     float box_margin[4];    // max |centre|, r_max^2, max |box coordinate|, 0 (rounded up)
     int32_t ncgroups;       // hierarchy groups, multiple of 16
     int32_t nbig;           // big-sphere groups tested for every ray
