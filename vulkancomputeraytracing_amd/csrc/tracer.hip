@@ -248,6 +248,17 @@ __device__ __forceinline__ float sqrt_unscaled(float x) {
     return __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
 }
 
+// Correctly rounded sqrt for any x: the unscaled sequence, and hipcc's full one in a real branch
+// for lanes outside [2^-96, inf] (tiny, zero, negative or NaN x).
+__device__ __forceinline__ float sqrt_fast(float x) {
+    float r = sqrt_unscaled(x);
+    if (!(x >= 0x1p-96f)) {
+        asm volatile("");
+        r = __builtin_sqrtf(x);
+    }
+    return r;
+}
+
 __device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a, float ya) {
 #ifdef VCRT_EXACT_CANDIDATE_OPS  // A/B builds: hipcc's full sequences
     return candidate_t(hb, disc, a);
@@ -1239,7 +1250,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             if (type == 1 || type == 2) {
                 const float r2 = rand_of_sin(s2);
                 const float r3 = rand_of_sin(s3);
-                const f3 u = normalize(mk(r1, r2, r3));  // random_in_unit_sphere(dir)
+                const f3 ru = mk(r1, r2, r3);  // random_in_unit_sphere(dir): normalize
+                const f3 u = divs(ru, sqrt_fast(dot(ru, ru)));
                 if (type == 1) {
                     d = add(normal, u);
                     atten = scale(param, mul(atten, albedo));
@@ -1256,7 +1268,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 if (dn > 0.0f) {
                     outward = neg(normal);
                     ni = param;
-                    cosine = __builtin_sqrtf(1.0f - param * param * (1.0f - dn * dn));
+                    cosine = sqrt_fast(1.0f - param * param * (1.0f - dn * dn));
                 } else {
                     outward = normal;
                     ni = 1.0f / param;
@@ -1267,7 +1279,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 const float dt = dot(d, outward);
                 const float disc = 1.0f - ni * ni * (1.0f - dt * dt);
                 if (disc > 0.0f) {
-                    const float sd = __builtin_sqrtf(disc);
+                    const float sd = sqrt_fast(disc);
                     refracted = sub(scale(ni, sub(d, scale(dt, outward))), scale(sd, outward));
                     reflect_prob = schlick(cosine, param);
                 }
@@ -1277,7 +1289,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             ++pass;
             if (pass >= p.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
         } else {
-            const float len = length(d);
+            const float len = sqrt_fast(dot(d, d));  // length(d)
             const float t = 0.5f * (d.y / len + 1.0f);
             const float om = 1.0f - t;
             contrib = mul(atten, mk(om + 0.5f * t, om + 0.7f * t, om + t));

@@ -191,8 +191,8 @@ VCRT_HD float sin_canonical(float xf) {
 // on |r| <= pi/2 (truncation < 2^-59.4), sign (-1)^k. For |x| < 2^19 and |r| >= 2^-12 the error
 // of s and that of sin_canonical's double result (2-term Cody-Waite reduction, fdlibm kernels)
 // are each below 2^-48 |sin x|; if s lies farther than 2^-44 |s| from every fp32 rounding
-// boundary, both round to the same float f. Otherwise (|r| < 2^-12, |x| >= 2^19, f a power of
-// two, or s near a boundary: ~2e-4 of the calls) the lane takes sin_canonical.
+// boundary, both round to the same float f. Otherwise (|r| < 2^-12, |x| >= 2^19, or s near a
+// boundary: ~2e-4 of the calls) the lane takes sin_canonical.
 // tests/test_gpu_parity.py::test_sin_fast_exhaustive compares the two on all 2^32 inputs.
 // A double constant materialised in an SGPR pair where it is used: plain literals get hoisted
 // out of the tracer's loops into VGPR pairs, which then spill (v_fma_f64 takes no 64-bit
@@ -215,9 +215,15 @@ __device__ __forceinline__ double fma_vvs(double a, double b, double c) {
     return d;
 }
 
+// Round 2: k by the 1.5 * 2^52 shifter (t = x / pi + 1.5 * 2^52 in one FMA: t's last mantissa
+// bit is k's parity, which flips the sign), and the boundary test on s's own mantissa: in s's
+// binade the fp32 rounding boundaries sit where the 29 bits below fp32 precision equal 2^28, so
+// s is accepted when those bits differ from 2^28 by more than 2^9 units of s's last place
+// (2^9 ulp_double(s) >= 2^-44 |s|, the margin above; binade ends need no special case).
 __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
     const double x = (double)xf;
-    const double k = __builtin_rint(x * VCRT_DC(0.31830988618379067154));
+    const double t = __builtin_fma(x, VCRT_DC(0.31830988618379067154), VCRT_DC(0x1.8p52));
+    const double k = t - VCRT_DC(0x1.8p52);
     double r = __builtin_fma(-k, VCRT_DC(0x1.921fb544p+1), x);
     r = __builtin_fma(-k, VCRT_DC(0x1.0b4611a626331p-33), r);
     const double r2 = r * r;
@@ -232,15 +238,13 @@ __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
     p = fma_vvs(p, r2, VCRT_DC(0x1.1111111111111p-7));
     p = fma_vvs(p, r2, VCRT_DC(-0x1.5555555555555p-3));
     double s = __builtin_fma(r * r2, p, r);
-    if ((int)k & 1) s = -s;
-    const float f = (float)s;
-    const uint32_t fb = __builtin_bit_cast(uint32_t, f);
-    // distance from s to the nearest rounding boundary of f (f normal: |f| > 2^-13)
-    const double half_ulp = __builtin_ldexp(1.0, __builtin_amdgcn_frexp_expf(f) - 25);
-    const double margin = half_ulp - __builtin_fabs(s - (double)f);
-    out = f;
+    const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+    const uint64_t sb = __builtin_bit_cast(uint64_t, s) ^ (tb << 63);  // (-1)^k
+    out = (float)__builtin_bit_cast(double, sb);
+    // bits 28..0 of s's mantissa (|s| >= 2^-13: normal in both formats)
+    const uint32_t below = (uint32_t)sb & 0x1FFFFFFFu;
     const bool ok = __builtin_fabsf(xf) < 0x1p19f && __builtin_fabs(r) >= 0x1p-12 &&
-                    (fb & 0x7FFFFFu) != 0u && margin > 0x1p-44 * __builtin_fabs(s);
+                    below - (0x10000000u - 0x200u) > 0x400u;
 #if VCRT_SINSB
     __builtin_amdgcn_sched_barrier(0);  // one evaluation at a time: the three rand() calls of a
                                         // diffuse hit interleaved would spill VGPRs
