@@ -65,7 +65,7 @@ struct RendererState {
     float4* d_geom = nullptr;  // pair-SoA groups of four (+1 padding group)
     float4* d_center_radius = nullptr;
     float4* d_shade = nullptr;
-    float* d_material = nullptr;
+    float4* d_material = nullptr;  // (material id, 1 / param, Schlick r0^2, 0) per sphere
     // culled-scan tables (cluster.hpp); ncgroups == 0 when culling does not apply
     int32_t ncgroups = 0, ncbig = 0;
     float cmargin[4] = {0, 0, 0, 0};  // box margin constants (CullTables::margin)
@@ -569,12 +569,17 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         base[6 + e] = r2;
     }
     std::vector<float4> cr(count), shade(count);
-    std::vector<float> mat(count);
+    std::vector<float4> mat(count);
     for (int32_t i = 0; i < count; i++) {
         const vcrt_sphere& sp = spheres[i];
         cr[i] = make_float4(sp.center[0], sp.center[1], sp.center[2], sp.radius);
         shade[i] = make_float4(sp.colour[0], sp.colour[1], sp.colour[2], sp.texture[1]);
-        mat[i] = sp.texture[0];
+        // the glass scatter's two per-sphere quotients (textures.glsl:49-50, functions.glsl:58-60),
+        // fp32 and correctly rounded as the kernel would compute them
+        const float ior = sp.texture[1];
+        float r0 = (1.0f - ior) / (1.0f + ior);
+        r0 = r0 * r0;
+        mat[i] = make_float4(sp.texture[0], 1.0f / ior, r0, 0.0f);
     }
     vcrt::CullTables ct;
     vcrt::build_cull_tables(spheres, count, ct);
@@ -631,13 +636,13 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     if (count > 0) {
         VCRT_TRY(hipMalloc(&g.d_center_radius, sizeof(float4) * count));
         VCRT_TRY(hipMalloc(&g.d_shade, sizeof(float4) * count));
-        VCRT_TRY(hipMalloc(&g.d_material, sizeof(float) * count));
+        VCRT_TRY(hipMalloc(&g.d_material, sizeof(float4) * count));
         VCRT_TRY(hipMemcpy(g.d_center_radius, cr.data(), sizeof(float4) * count,
                            hipMemcpyHostToDevice));
         VCRT_TRY(
             hipMemcpy(g.d_shade, shade.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
         VCRT_TRY(
-            hipMemcpy(g.d_material, mat.data(), sizeof(float) * count, hipMemcpyHostToDevice));
+            hipMemcpy(g.d_material, mat.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
     }
     g.nspheres = count;
     g.stats.nspheres = count;

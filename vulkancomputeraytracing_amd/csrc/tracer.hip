@@ -1235,10 +1235,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         if (best >= 0) {
             const float4 cr = p.center_radius[best];
             const float4 sh = p.shade[best];
-            const float mat = p.material[best];
+            const float4 mat = p.material[best];
             const f3 point = add(scale(max_t, d), o);
             const f3 normal = divs(sub(point, mk(cr.x, cr.y, cr.z)), cr.w);
-            const int type = (int)mat;
+            const int type = (int)mat.x;
             const f3 albedo = mk(sh.x, sh.y, sh.z);
             const float param = sh.w;
             // rand(dir.xy), rand(dir.xz), rand(dir.yz) for lambertian/metal (functions.glsl:43),
@@ -1271,7 +1271,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     cosine = sqrt_fast(1.0f - param * param * (1.0f - dn * dn));
                 } else {
                     outward = normal;
-                    ni = 1.0f / param;
+                    ni = mat.y;  // 1.0f / param
                     cosine = -dn;
                 }
                 f3 refracted = mk(0.f, 0.f, 0.f);
@@ -1281,7 +1281,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 if (disc > 0.0f) {
                     const float sd = sqrt_fast(disc);
                     refracted = sub(scale(ni, sub(d, scale(dt, outward))), scale(sd, outward));
-                    reflect_prob = schlick(cosine, param);
+                    reflect_prob = schlick_r0(cosine, mat.z);  // schlick(cosine, param)
                 }
                 o = point;
                 d = (r1 < reflect_prob) ? reflected : refracted;

@@ -23,7 +23,8 @@ struct TraceParams {
     const float4* geom;           // pair-SoA sphere groups (+1 padding group), scan input
     const float4* center_radius;  // [n] (center.xyz, radius)           -- read once per hit
     const float4* shade;          // [n] (colour.rgb, texture.y = param)
-    const float* material;        // [n] texture.x = material id
+    const float4* material;       // [n] (texture.x = material id, 1 / texture.y, Schlick r0^2
+                                  //   of texture.y, 0): the glass quotients precomputed (fp32)
     const float2* jitter;  // [spp] (-0.5+rand(i,i), -0.5+rand(i+1,i+1)), shader.comp:48
     float4* out;           // rank-local framebuffer, rgba32f (layout above)
     double* accum;         // [local_tiles * 64][4] exact sums of the quantized chunk sums (r, g,

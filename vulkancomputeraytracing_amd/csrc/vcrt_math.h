@@ -305,6 +305,13 @@ VCRT_HD float schlick(float cosine, float ior) {
     return r0 + (1.0f - r0) * p5;
 }
 
+// schlick with r0 = ((1 - ior) / (1 + ior))^2 given (the same operations as schlick after it)
+VCRT_HD float schlick_r0(float cosine, float r0) {
+    float x = 1.0f - cosine;
+    float p5 = (x < 0.0f) ? __builtin_nanf("") : ((x * x) * (x * x)) * x;
+    return r0 + (1.0f - r0) * p5;
+}
+
 // ---------------------------------------------------------------------------------------
 // Accumulation (shader.comp:46-56: color.rgb += ray_color(...); color /= SPP). The reference
 // sums a pixel's samples in fp32 in sample order. The GPU splits them into work items of K
