@@ -62,6 +62,7 @@ struct RendererState {
     // scene
     int32_t nspheres = 0;
     bool scene_bounded = false;  // every |center|, radius <= 2^30: discriminants stay finite
+    bool radii_safe = false;     // every |radius| in [2^-40, 2^30] (kFlagRadiiSafe)
     float4* d_geom = nullptr;  // pair-SoA groups of four (+1 padding group)
     float4* d_center_radius = nullptr;
     float4* d_shade = nullptr;
@@ -649,10 +650,13 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     g.accumulated = 0;  // a new scene restarts progressive accumulation
     if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
     g.scene_bounded = true;
+    g.radii_safe = true;
     for (int32_t i = 0; i < count; i++) {
         const vcrt_sphere& sp = spheres[i];
         for (float v : {sp.center[0], sp.center[1], sp.center[2], sp.radius})
             if (!(std::fabs(v) <= 0x1p30f)) g.scene_bounded = false;  // also rejects NaN
+        if (!(std::fabs(sp.radius) >= 0x1p-40f && std::fabs(sp.radius) <= 0x1p30f))
+            g.radii_safe = false;
     }
     return VCRT_SUCCESS;
 }
@@ -725,6 +729,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.chunk = g.chunk;
         p.nchunks = g.nchunks;
         p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
+                  (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
                   (g.direct ? vcrt::kFlagDirect : 0u);
         p.spp_total = static_cast<float>(spp_total);
         const std::array<float, 12> cam = camera_array();

@@ -1237,7 +1237,18 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             const float4 sh = p.shade[best];
             const float4 mat = p.material[best];
             const f3 point = add(scale(max_t, d), o);
-            const f3 normal = divs(sub(point, mk(cr.x, cr.y, cr.z)), cr.w);
+            // normal = (point - centre) / radius: the unscaled division with one reciprocal
+            // (exact: candidate_t_fast's argument) for numerators and radius in [2^-40, 2^30]
+            // (the radius by a host flag), else hipcc's full division in a real branch
+            const f3 pcv = sub(point, mk(cr.x, cr.y, cr.z));
+            const float yr = recip_a(cr.w);
+            f3 normal = mk(div_a(pcv.x, cr.w, yr), div_a(pcv.y, cr.w, yr), div_a(pcv.z, cr.w, yr));
+            const float nmin = fminf(fminf(fabsf(pcv.x), fabsf(pcv.y)), fabsf(pcv.z));
+            const float nmax = fmaxf(fmaxf(fabsf(pcv.x), fabsf(pcv.y)), fabsf(pcv.z));
+            if (!((p.flags & kFlagRadiiSafe) != 0u && nmin >= 0x1p-40f && nmax <= 0x1p30f)) {
+                asm volatile("");
+                normal = divs(pcv, cr.w);
+            }
             const int type = (int)mat.x;
             const f3 albedo = mk(sh.x, sh.y, sh.z);
             const float param = sh.w;

@@ -77,6 +77,8 @@ constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 constexpr uint32_t kFlagChunkMinor = 8u;  // a block's 64 items run chunk-minor: all chunks of
                                           // 64 / nchunks pixels (else one chunk of 64 pixels)
+constexpr uint32_t kFlagRadiiSafe = 16u;  // every |radius| in [2^-40, 2^30] (host-checked):
+                                         // shading's (p - c) / r may take the unscaled division
 constexpr uint32_t kFlagDirect = 4u;  // one work item per pixel and frame, not progressive: the
                                       // lane writes the pixel itself (no sums, no resolve pass)
 
