@@ -187,9 +187,10 @@ VCRT_HD float sin_canonical(float xf) {
 // (sin_canonical evaluates both fdlibm kernels under divergence, since the quadrant varies per
 // lane), accepted when it provably rounds to the same fp32 as sin_canonical, else
 // sin_canonical itself. Fast value s: x reduced modulo pi (k = rint(x / pi); r = x - k pi with
-// pi split as pi_hi (33 bits: k pi_hi exact for |k| < 2^20) + pi_mid, FMAs), then Taylor to r^21
-// on |r| <= pi/2 (truncation < 2^-59.4), sign (-1)^k. For |x| < 2^19 and |r| >= 2^-12 the error
-// of s and that of sin_canonical's double result (2-term Cody-Waite reduction, fdlibm kernels)
+// pi split as pi_hi (33 bits: k pi_hi exact for |k| < 2^20) + pi_mid, FMAs), then Taylor to
+// r^19 on |r| <= pi/2 (truncation < 2^-51.8 |sin r|), sign (-1)^k. For |x| < 2^19 and
+// |r| >= 2^-12 the error of s and that of sin_canonical's double result (2-term Cody-Waite
+// reduction, fdlibm kernels)
 // are each below 2^-48 |sin x|; if s lies farther than 2^-44 |s| from every fp32 rounding
 // boundary, both round to the same float f. Otherwise (|r| < 2^-12, |x| >= 2^19, or s near a
 // boundary: ~2e-4 of the calls) the lane takes sin_canonical.
@@ -227,8 +228,7 @@ __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
     double r = __builtin_fma(-k, VCRT_DC(0x1.921fb544p+1), x);
     r = __builtin_fma(-k, VCRT_DC(0x1.0b4611a626331p-33), r);
     const double r2 = r * r;
-    double p = VCRT_DC(0x1.71b8ef6dcf572p-66);  // (-1)^j / (2j+1)!, j = 10 .. 1
-    p = fma_vvs(p, r2, VCRT_DC(-0x1.2f49b46814157p-57));
+    double p = VCRT_DC(-0x1.2f49b46814157p-57);  // (-1)^j / (2j+1)!, j = 9 .. 1
     p = fma_vvs(p, r2, VCRT_DC(0x1.952c77030ad4ap-49));
     p = fma_vvs(p, r2, VCRT_DC(-0x1.ae7f3e733b81fp-41));
     p = fma_vvs(p, r2, VCRT_DC(0x1.6124613a86d09p-33));
