@@ -117,18 +117,21 @@ RendererState g;
     } while (0)
 
 // Samples per work item when the caller leaves it to us: 64, halved (down to 16) while the
-// largest rank's share of the frame would be fewer than 2^23 items, so every lane of the
-// persistent grid (~330k lanes on MI355X) still gets ~25 items and the drain at the end of the
-// queue stays short; at least spp / 512 (at most kAccumMaxChunks chunks per pixel). Smaller
-// items cost more than they save in balance: every item start and end (slot fetch, pixel
-// set-up, three f64 atomics whose completion later loads wait for) is paid by the whole wave.
-// Measured: C4 on one GPU 159.9 / 151.9 / 148.8 / ~147 ms at K = 8 / 16 / 32 /
-// 64, its 8-way shards 20.6 / 20.4 / 21.9 ms at K = 8 / 16 / 32; C2 2.26 / 1.63 / 2.04 ms at
-// K = 4 / 16 / 64. All ranks of a frame use the same K (the largest rank's share decides), so
-// a sharded frame equals a one-GPU render with that K bit for bit.
+// largest rank's share of the frame would be fewer than kChunkItems = 2^25 - 2^22 items (~90 per
+// lane of the persistent grid, ~330k lanes on MI355X), so the drain at the end of the queue
+// stays short; at least spp / 512 (at most kAccumMaxChunks chunks per pixel). Smaller items cost
+// more than they save in balance: every item start and end (slot fetch, pixel set-up, three f64
+// atomics whose completion later loads wait for) is paid by the whole wave. Measured at round 2
+// (profiles/r02_chunk_sweep.txt; per-rank kernel ms at K = 8 / 16 / 32 / 64): C4 on
+// one GPU 153.6 / 144.4 / 141.2 / 139.7 -> 64; its 2-way shards 76.7 / 72.7 / 71.5 / 73.4 -> 32;
+// 4-way 38.7 / 36.9 / 37.6 / 41.2 -> 16; 8-way 19.8 / 19.5 / 20.9 / 25.5 -> 16; C3 36.8 / 37.5 /
+// 41.4 at K = 16 / 32 / 64 -> 16. All ranks of a frame use the same K (the largest rank's share
+// decides), so a sharded frame equals a one-GPU render with that K bit for bit.
+constexpr uint64_t kChunkItems = (uint64_t{1} << 25) - (uint64_t{1} << 22);
+
 int32_t default_chunk(uint64_t rank_slots, int32_t spp) {
     int32_t k = kDefaultChunk;
-    while (k > 16 && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < (uint64_t{1} << 23))
+    while (k > 16 && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems)
         k /= 2;
     const int32_t k_min = (spp + vcrt::kAccumMaxChunks - 1) / vcrt::kAccumMaxChunks;
     return std::max(k, k_min);
