@@ -153,7 +153,7 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
     assert st["segments"] == segs
     assert st["tables_in_lds"] == (tables == "lds" and scene == "final")
     if not st["tables_in_lds"]:
-        assert st["lds_bytes"] == 4 * 6400 and st["block_threads"] == 256
+        assert st["lds_bytes"] == 4 * 6912 and st["block_threads"] == 256
 
 
 def culling_torture_scene():

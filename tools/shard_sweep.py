@@ -14,9 +14,10 @@ p.add_argument("--spp", type=int, default=1024)
 p.add_argument("--worlds", default="2,4,8")
 p.add_argument("--chunk", type=int, default=0)
 p.add_argument("--variant", type=int, default=0)
+p.add_argument("--code-object", default=None)
 a = p.parse_args()
 base = dict(width=1920, height=1080, samples_per_pixel=a.spp, max_depth=10, device=0,
-            accumulate_chunk=a.chunk, kernel_variant=a.variant)
+            accumulate_chunk=a.chunk, kernel_variant=a.variant, code_object_path=a.code_object)
 # steady state: the second frame of each renderer (the first after Begin runs ~5% slower)
 with vc.Renderer(vc.RenderDesc(**base), "final") as r:
     r.draw_next_frame()

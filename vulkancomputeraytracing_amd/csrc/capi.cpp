@@ -74,6 +74,7 @@ struct RendererState {
     float4* d_cbound = nullptr;
     float4* d_cbound_nf = nullptr;
     float4* d_cnode = nullptr;
+    float4* d_cnode_nf = nullptr;  // node-pair boxes, near/far layout, padded to whole chunks
     float4* d_ctop = nullptr;
     uint32_t* d_prim_info = nullptr;  // camera-ray tile lists (primary.cpp), flat scan only
     uint16_t* d_prim_ids = nullptr;
@@ -221,6 +222,7 @@ void free_scene() {
     if (g.d_cbound) (void)hipFree(g.d_cbound);
     if (g.d_cbound_nf) (void)hipFree(g.d_cbound_nf);
     if (g.d_cnode) (void)hipFree(g.d_cnode);
+    if (g.d_cnode_nf) (void)hipFree(g.d_cnode_nf);
     if (g.d_ctop) (void)hipFree(g.d_ctop);
     if (g.d_prim_info) (void)hipFree(g.d_prim_info);
     if (g.d_prim_ids) (void)hipFree(g.d_prim_ids);
@@ -232,6 +234,7 @@ void free_scene() {
     g.d_cbound = nullptr;
     g.d_cbound_nf = nullptr;
     g.d_cnode = nullptr;
+    g.d_cnode_nf = nullptr;
     g.d_ctop = nullptr;
     g.ncgroups = 0;
     g.ncbig = 0;
@@ -609,6 +612,13 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
                            hipMemcpyHostToDevice));
         // near/far layout of the group boxes for the flat scan (vcrt_kernel_abi.h, cbound_nf)
         VCRT_TRY(upload_near_far(ct.bound, &g.d_cbound_nf));
+        {
+            // the flat scan's chunk passes read a chunk's 4 node pairs: pad to whole chunks
+            std::vector<float> nodes = ct.node;
+            const size_t pairs = nodes.size() / 16, padded = (pairs + 3) / 4 * 4;
+            nodes.resize(padded * 16, 0.0f);
+            VCRT_TRY(upload_near_far(nodes, &g.d_cnode_nf));
+        }
         VCRT_TRY(hipMemcpy(g.d_cnode, ct.node.data(), sizeof(float) * ct.node.size(),
                            hipMemcpyHostToDevice));
         g.ncgroups = ct.ngroups;
@@ -712,6 +722,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.cbound = g.d_cbound;
         p.cbound_nf = g.d_cbound_nf;
         p.cnode = g.d_cnode;
+        p.cnode_nf = g.d_cnode_nf;
         p.ctop = g.d_ctop;
         p.prim_info = g.d_prim_info;
         p.prim_ids = g.d_prim_ids;

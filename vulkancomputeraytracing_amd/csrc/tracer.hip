@@ -624,9 +624,10 @@ __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
 
 // ---- flattened scan (variant CULL_FLAT) ------------------------------------------------------
 // The per-lane scan runs each level as many wave passes as its busiest lane needs (twice the
-// mean). Here the work items of the two per-lane levels and of the root evaluation are kept as
-// three per-wave stacks in LDS and dealt to the wave's live lanes a full wave at a time, each
+// mean). Here the work items of the per-lane levels and of the root evaluation are kept as
+// four per-wave stacks in LDS and dealt to the wave's live lanes a full wave at a time, each
 // lane working on another lane's ray (fetched with ds_bpermute):
+//   chunk (owner, chunk)               -> tests the chunk's <= 8 node bounds -> node entries
 //   node  (owner, node)                -> tests the node's 8 group bounds -> group entries
 //   group (owner, group)               -> exact test of the 4 members     -> candidate entries
 //   cand  (owner, group, member)       -> the accepted root, into the owner's key
@@ -638,7 +639,12 @@ __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
 // minimum of (t, index) is what `consider` computes, since t > 0 orders like its bit pattern.
 // A pass pushes onto the next stack only while that stack holds < nact <= 64 entries (full
 // passes run deepest stack first; the final drain's partial passes run top-down), which bounds
-// every stack: < 64 left over + at most 8 x 64 (node, group) or 4 x 64 (cand) pushed by one pass.
+// every stack: < 64 left over + at most 8 x 64 (node, group) or 4 x 64 (cand) pushed by one pass;
+// chunk entries (one per lane and chunk) are pushed between drains, onto < 64 left over.
+// (Round 2: the chunk level was wave-uniform -- every lane tested the nodes of every chunk some
+// lane needed, with per-lane min/max box tests on scalar-loaded boxes; as passes the nodes are
+// tested only for the lanes that need the chunk, by the near/far box test.)
+constexpr int kChunkCap = 128;
 constexpr int kNodeCap = 576;
 constexpr int kGroupCap = 576;
 constexpr int kCandCap = 320;
@@ -660,6 +666,7 @@ struct WaveScratch {
     uint32_t cand[kCandCap];     // group entry << 2 | member
     entry_t group[kGroupCap];    // owner << kShift | group
     entry_t node[kNodeCap];      // owner << kShift | node
+    entry_t chunk[kChunkCap];    // owner << kShift | chunk (64 groups)
 };
 static_assert(sizeof(WaveScratch<false>) == kWaveScratchBytes, "host LDS size");
 static_assert(sizeof(WaveScratch<true>) == kWaveScratchBytesWide, "host LDS size");
@@ -745,15 +752,18 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 template <int kKind, bool kWide>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
                                           uint32_t rank, uint32_t lane, WaveScratch<kWide>* ws,
-                                          const float4* tbound, const GroupTab<kWide>& tg,
-                                          const FlatRay& my) {
+                                          const float4* tbound, const float4* tnode, uint32_t ncg,
+                                          const GroupTab<kWide>& tg, const FlatRay& my) {
     using F = FlatFmt<kWide>;
     using entry_t = typename F::entry_t;
     const uint32_t m = min(n, nact), top = n - m;
     n = top;
     const bool act = rank < m;
-    if constexpr (kKind == 2) {  // node: the 8 group bounds of (owner, node)
-        const uint32_t e = act ? (uint32_t)ws->node[top + rank] : (lane << F::kShift);
+    if constexpr (kKind == 2 || kKind == 3) {  // node: the 8 group bounds of (owner, node);
+                                               // chunk: the <= 8 node bounds of (owner, chunk)
+        const uint32_t e = act ? (uint32_t)(kKind == 2 ? ws->node[top + rank]
+                                                       : ws->chunk[top + rank])
+                               : (lane << F::kShift);
         const int src = (int)(e >> F::kShift) << 2;
         BoxRay r;
         const float ix = from_lane(src, my.br.ix.x), iy = from_lane(src, my.br.iy.x),
@@ -769,12 +779,16 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         r.cz = (v2f){cz, cz};
         r.c1 = (v2f){c1, c1};
         r.c2 = (v2f){c2, c2};
-        const float4* gb = tbound + 20u * (e & F::kMask);  // 4 pairs x 80 B
+        // 4 pairs x 80 B: a node's 8 groups, or a chunk's 8 nodes (padded past the last one)
+        const float4* gb = (kKind == 2 ? tbound : tnode) + 20u * (e & F::kMask);
         const NearFarAddr na = near_far_addr(gb, ix, iy, iz);
         uint32_t gout = 0;
 #pragma unroll
         for (int k = 3; k >= 0; k--) gout = push_bound_pair_nf(gout, r, na, 80 * k);
-        uint32_t need = act ? (~gout & 0xffu) : 0u;
+        uint32_t valid = 0xffu;
+        if constexpr (kKind == 3)  // the last chunk may hold fewer than 8 nodes
+            valid = (1u << min(8u, (ncg >> 3) - 8u * (e & F::kMask))) - 1u;
+        uint32_t need = act ? (~gout & valid) : 0u;
         uint32_t tot;
         uint32_t pos = pushed + wave_prefix<4>((uint32_t)__popc(need), tot);
         pushed += tot;
@@ -783,7 +797,10 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
             do {
                 const uint32_t k = (uint32_t)__builtin_ctz(need);
                 need &= need - 1;
-                ws->group[pos++] = (entry_t)(tag | k);
+                if constexpr (kKind == 2)
+                    ws->group[pos++] = (entry_t)(tag | k);
+                else
+                    ws->node[pos++] = (entry_t)(tag | k);
             } while (need);
         }
     } else if constexpr (kKind == 1) {  // group: exact test of the 4 members for the owner's ray
@@ -854,24 +871,25 @@ struct PhaseTicks {
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
 
 struct FlatStacks {  // wave-uniform stack heights
-    uint32_t cand, group, node;
+    uint32_t cand, group, node, chunk;
 };
 
 template <bool kStats, bool kWide>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
                                            WaveScratch<kWide>* ws, FlatStacks& h,
-                                           const float4* tbound,
+                                           const float4* tbound, const float4* tnode, uint32_t ncg,
                                            const GroupTab<kWide>& tg, const FlatRay& my,
                                            uint32_t& n_groups, uint32_t& n_bounds,
                                            PhaseTicks& pt) {
-    uint32_t nc = h.cand, ng = h.group, nn = h.node;
+    uint32_t nc = h.cand, ng = h.group, nn = h.node, nk = h.chunk;
     for (;;) {
         __builtin_amdgcn_wave_barrier();  // the entries were written by other lanes
         uint64_t t0 = 0;
         if constexpr (kStats) {
             t0 = ticks();
             const uint32_t n = nc >= nact ? nc : ng >= nact ? ng : nn >= nact ? nn
-                             : th == 1u ? (nn ? nn : ng ? ng : nc) : 0u;
+                             : nk >= nact ? nk
+                             : th == 1u ? (nk ? nk : nn ? nn : ng ? ng : nc) : 0u;
             if (n) {
                 pt.pass_entries += min(n, nact);
                 pt.pass_lanes += nact;
@@ -880,29 +898,34 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
             }
         }
         // full passes first, deepest stack first; then (final drain only) the partial passes
-        // top-down, nodes before groups before candidates, so that each level's remainder
-        // joins the next level's before that one runs: ~3 partial passes per segment instead
-        // of a cascade. A pass onto a stack runs only while that stack holds < nact <= 64
+        // top-down, chunks before nodes before groups before candidates, so that each level's
+        // remainder joins the next level's before that one runs: ~3 partial passes per segment
+        // instead of a cascade. A pass onto a stack runs only while that stack holds < nact <= 64
         // entries, which keeps the caps (see kNodeCap).
         int kind = -1;
         if (nc >= nact) kind = 0;
         else if (ng >= nact) kind = 1;
         else if (nn >= nact) kind = 2;
-        else if (th == 1u) kind = nn ? 2 : ng ? 1 : nc ? 0 : -1;
+        else if (nk >= nact) kind = 3;
+        else if (th == 1u) kind = nk ? 3 : nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
-            flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tg, my);
+            flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (kind == 1) {
             ++n_groups;
-            flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tg, my);
+            flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
             n_bounds += 8;
-            flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tg, my);
+            flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
+        } else if (kind == 3) {
+            n_bounds += 8;
+            flat_pass<3, kWide>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            if constexpr (kStats) pt.levels += ticks() - t0;
         } else {
             break;
         }
@@ -910,6 +933,7 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
     h.cand = nc;
     h.group = ng;
     h.node = nn;
+    h.chunk = nk;
 }
 
 template <bool kStats, bool kWide>
@@ -953,7 +977,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     const uint64_t live = __ballot(1);
     const uint32_t nact = (uint32_t)__popcll(live), rank = lanes_below(live);
     ws->key[lane] = pack_hit(max_t, best);
-    FlatStacks h = {0u, 0u, 0u};
+    FlatStacks h = {0u, 0u, 0u, 0u};
     // A camera ray (primary) whose tile has a group list (primary.cpp) pushes those groups
     // straight onto the group stack and skips the chunk and node levels: the list holds every
     // group such a ray may need (at most 8 per lane: at most 512 entries on the empty stack).
@@ -985,8 +1009,19 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                 n_bounds += 2;
             }
             const bool in_chunk = !listed && ((tops >> ((base >> 6) & 1)) & 1u) != 0;
-            if (__ballot(in_chunk) == 0) continue;
-            // level 1, wave-uniform: nodes of this chunk, per-lane bits -> node entries
+            const uint64_t want = __ballot(in_chunk);
+            if (want == 0) continue;
+            if constexpr (kWide) {
+            // level 1 (global tables: many chunks): a chunk entry per lane whose ray may meet
+            // the chunk; chunk passes test its nodes for that lane alone
+            if (in_chunk)
+                ws->chunk[h.chunk + lanes_below(want)] = (typename FlatFmt<kWide>::entry_t)(
+                    (lane << FlatFmt<kWide>::kShift) | ((uint32_t)base >> 6));
+            h.chunk += (uint32_t)__popcll(want);
+            if constexpr (kStats) pt.push += ticks() - t0;
+            } else {
+            // level 1 (LDS tables: two chunks at the final scene), wave-uniform: nodes of this
+            // chunk, per-lane bits -> node entries
             const int nn = min(8, (ncg - base) >> 3);
             uint32_t out = 0;
             cfloat4* nb = node + 4 * (base >> 4);
@@ -1015,10 +1050,10 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                 } while (nodes);
             }
             if constexpr (kStats) pt.push += ticks() - t0;
+            }
         }
-        flat_drain<kStats, kWide>(th, nact, rank, lane, ws, h, tbound, tg, my, n_groups,
-                                  n_bounds,
-                           pt);
+        flat_drain<kStats, kWide>(th, nact, rank, lane, ws, h, tbound, p.cnode_nf,
+                                  (uint32_t)ncg, tg, my, n_groups, n_bounds, pt);
         if (base >= ncg) break;
     }
     __builtin_amdgcn_wave_barrier();

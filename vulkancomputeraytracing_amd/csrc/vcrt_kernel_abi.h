@@ -46,6 +46,9 @@ struct TraceParams {
                               //   x then y then z, then (K0,K1) -- 80 B per pair
     const float4* cnode;    // [ncgroups / 16 * 4] boxes of node pairs (8 groups per node)
     const float4* ctop;     // boxes of pairs of 64-group chunks, same form
+    const float4* cnode_nf;  // [ceil(ncgroups / 64) * 4 * 5] the node-pair boxes in the near/far
+                             //   layout of cbound_nf, padded to whole chunks (the flat scan's
+                             //   chunk passes)
     const uint32_t* prim_info;  // [4 local_tiles] camera-ray group list of each 4x4 quarter
                                 //   (4 lt + 2 qy + qx) of each local tile: offset << 4 |
                                 //   count (count <= 8; 15 = none), or null
@@ -71,8 +74,8 @@ struct TraceParams {
 };
 
 constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
-constexpr uint32_t kWaveScratchBytes = 4096;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
-constexpr uint32_t kWaveScratchBytesWide = 6400;  // the same with 32-bit entries (global tables)
+constexpr uint32_t kWaveScratchBytes = 4352;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
+constexpr uint32_t kWaveScratchBytesWide = 6912;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 constexpr uint32_t kFlagChunkMinor = 8u;  // a block's 64 items run chunk-minor: all chunks of
