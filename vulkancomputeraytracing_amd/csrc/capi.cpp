@@ -56,7 +56,8 @@ struct RendererState {
                   k_trace_cull_flat_global_stats = nullptr;
     int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
-    bool debug_stats = false;
+    int debug_stats = 0;  // 1: the stats kernels; 2: the product kernels with a debug buffer
+                          //    (builds with VCRT_WAVE_END_TIMES record wave start/end times)
     uint32_t work_flags = 0;
     void* d_debug = nullptr;
     // scene
@@ -519,7 +520,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         if ((r = to_vk(hipMemset(g.d_accum, 0, bytes))) != VK_SUCCESS) return fail(r);
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
-    if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e);
     if (const char* e = std::getenv("VCRT_PRIMARY_LISTS")) g.primary_lists = std::atoi(e) != 0;
     if (const char* e = std::getenv("VCRT_CULL_LANE_TABLES"))
         g.cull_lane_tables = std::strcmp(e, "lds") == 0 ? 1 : std::strcmp(e, "global") == 0 ? 2 : 0;
@@ -820,11 +821,11 @@ vcrt_result vcrt_draw_next_frame(void) {
             fs = g.k_trace_cull_lane_stats;
             fname = "vcrt_trace_cull_lane";
         }
-        if (g.debug_stats) f = fs;
+        if (g.debug_stats == 1) f = fs;
         // the stage names the entry point this draw dispatches (Shader.cpp:89 names "main")
         g.stage.pName = fname;
         std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s%s", fname,
-                      g.debug_stats ? "_stats" : "");
+                      g.debug_stats == 1 ? "_stats" : "");
         int per_cu = g.desc.blocks_per_cu;
         if (per_cu <= 0) {
             per_cu = 0;
@@ -839,6 +840,7 @@ vcrt_result vcrt_draw_next_frame(void) {
             VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
         if (g.debug_stats) {
             unsigned long long init[32] = {0, 0, 0, 0, 0, ~0ull};
+            if (g.debug_stats == 2) init[9] = init[10] = ~0ull;  // wave times: minima
             VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
                                     g.stream));
         }

@@ -1257,6 +1257,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     PhaseTicks pt;                         // stats builds: wave clock per phase
     uint64_t t_begin = 0;
     if constexpr (kStats) t_begin = ticks();
+#ifdef VCRT_WAVE_END_TIMES
+    const unsigned long long t_start_rt = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t_drained_rt = ~0ull;
+#endif
     // the wave's current block of items (wave-uniform); 64 = exhausted, fetch a new one
     const uint32_t total_blocks = p.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
@@ -1401,6 +1405,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 if ((int)lane == leader) b = atomicAdd(p.work, 1u);
                 b = __builtin_amdgcn_readfirstlane(__shfl(b, leader));
                 if (b >= total_blocks) {  // queue drained: lanes still wanting work are done
+#ifdef VCRT_WAVE_END_TIMES
+                    if (t_drained_rt == ~0ull) t_drained_rt = __builtin_amdgcn_s_memrealtime();
+#endif
                     if (need) done = true;
                     break;
                 }
@@ -1605,6 +1612,19 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
 
     }
 
+#ifdef VCRT_WAVE_END_TIMES  // diagnostics builds (VCRT_DEBUG_STATS=2): when waves start, end,
+                            // and see the queue drained (s_memrealtime, 100 MHz)
+    if (!kStats && lane == 0 && p.debug) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        atomicMax(p.debug + 4, t);
+        atomicMin(p.debug + 5, t);
+        atomicAdd(p.debug + 6, t >> 8);
+        atomicAdd(p.debug + 7, 1ull);
+        atomicMin(p.debug + 9, t_start_rt);
+        atomicMin(p.debug + 10, t_drained_rt);
+        atomicAdd(p.debug + 11, t_drained_rt >> 8);
+    }
+#endif
     // one segment-counter atomic per wave
     unsigned long long total = segs;
 #pragma unroll
