@@ -1247,6 +1247,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
 
     bool done = false, need = true;
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
+    // flat scan: a main-scan hit waits for the next iteration's shading (pend_t, pend_best;
+    // pend_best < 0: none), which it shares with that iteration's camera rays
+    float pend_t = 0.0f;
+    int pend_best = -1;
     int sample = 0, sample_end = 0, pass = 0;
     uint32_t q = 0;
     uint32_t pxy = 0;  // the item's pixel: y << 16 | x
@@ -1483,6 +1487,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             const bool cam_now = fresh && (inf & 15u) != 15u && (p.flags & kFlagSceneBounded) != 0 &&
                                  aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
+            float mt = 1e5f;
+            int bst = -1;
             if (__ballot(cam_now)) {
                 if constexpr (kStats) {
                     ++pt.cam_entries;
@@ -1490,8 +1496,6 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     pt.cam_live += (uint64_t)__popcll(__ballot(1));
                 }
                 uint32_t iters = 0, roots = 0;
-                float mt = 1e5f;
-                int bst = -1;
                 if (cam_now) {
                     ++segs;
                     // A camera ray starts at the camera centre: its members' oc and cc come
@@ -1555,8 +1559,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 }
                 // issued work: the big list and the loop's passes, per wave
                 w_groups += (uint64_t)p.nbig + wave_max_small<4>(iters);
-                if (cam_now) fresh = shade_and_advance(mt, bst);
             }
+            // One shading for the camera rays just traced and the main-scan hits of the last
+            // iteration: the hit branches run once per iteration for both (a lane has at most
+            // one of them; each lane's own sequence of operations is unchanged).
+            const bool pending = pend_best >= 0;
+            if (pending) {
+                mt = pend_t;
+                bst = pend_best;
+                pend_best = -1;
+            }
+            if (cam_now || pending) fresh = shade_and_advance(mt, bst);
             if constexpr (kStats) pt.cam += ticks() - t_cam;
             if (need) continue;  // that segment finished the lane's chunk
         }
@@ -1607,7 +1620,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             t_shade = ticks();
             pt.shade_hits += (uint64_t)__popcll(__ballot(best >= 0));
         }
-        fresh = shade_and_advance(max_t, best);
+        if constexpr (kCull == 4 || kCull == 5) {
+            if (best >= 0) {  // a hit: shaded with the next iteration's camera rays
+                pend_t = max_t;
+                pend_best = best;
+                fresh = false;  // the ray is traced (it may have been a camera ray)
+            } else {
+                fresh = shade_and_advance(max_t, best);  // the sky
+            }
+        } else {
+            fresh = shade_and_advance(max_t, best);
+        }
         if constexpr (kStats) pt.shade += ticks() - t_shade;
 
     }
