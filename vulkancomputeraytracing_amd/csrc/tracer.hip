@@ -1254,8 +1254,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     int sample = 0, sample_end = 0, pass = 0;
     uint32_t q = 0;
     uint32_t pxy = 0;  // the item's pixel: y << 16 | x
-    f3 pc = mk(0.f, 0.f, 0.f), o = pc, d = pc, atten = pc, acc = pc;
-    unsigned long long segs = 0;
+    f3 o = mk(0.f, 0.f, 0.f), d = o, atten = o, acc = o;
+    // shader.comp:43  pixel00 + x*delta_u + y*delta_v, recomputed from pxy at each sample start
+    // (three VGPRs fewer across the loop than keeping it)
+    auto pixel_corner = [&]() {
+        return add(add(p00, scale((float)(pxy & 0xffffu), du)), scale((float)(pxy >> 16), dv));
+    };
+    uint32_t segs = 0;  // this lane's segments (< 2^32: ~2.4e5 per lane at the C5 workload)
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
     uint64_t w_groups = 0, w_bounds = 0;  // per wave (uniform): sphere groups / bounds tested
     PhaseTicks pt;                         // stats builds: wave clock per phase
@@ -1380,7 +1385,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 need = true;
             } else {
                 const float2 jt = p.jitter[sample];
-                const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
+                const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
                 o = cam;
                 d = sub(ps, cam);
                 atten = mk(1.f, 1.f, 1.f);
@@ -1449,13 +1454,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             q = g_lt * 64u + g_slot;
             pxy = (g_py << 16) | g_px;
             // shader.comp:43  pixel00 + x*delta_u + y*delta_v
-            pc = add(add(p00, scale((float)g_px, du)), scale((float)g_py, dv));
             acc = mk(0.f, 0.f, 0.f);
             sample = (int)(g_chunk * (uint32_t)p.chunk);
             sample_end = min(sample + p.chunk, p.spp);
             // first camera ray of the chunk, shader.comp:48-52
             const float2 jt = p.jitter[sample];
-            const f3 ps = add(pc, add(scale(jt.x, du), scale(jt.y, dv)));
+            const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
             o = cam;
             d = sub(ps, cam);
             atten = mk(1.f, 1.f, 1.f);
@@ -1649,7 +1653,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     }
 #endif
     // one segment-counter atomic per wave
-    unsigned long long total = segs;
+    unsigned long long total = segs;  // widened before the wave sum
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
     if (lane == 0 && total) atomicAdd(p.segments, total);
