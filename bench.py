@@ -170,17 +170,19 @@ def validate(args, got, st, device, world):
     out = {}
     rows = list(range(args.height // (2 * args.validate_rows), args.height,
                       max(1, args.height // args.validate_rows)))[:args.validate_rows]
-    cfg = o.config(args.width, args.height, args.spp, args.depth, chunk=st["accumulate_chunk"])
+    cfg = o.config(args.width, args.height, args.spp, args.depth, **o.partition(st))
     want = np.stack([o.render(cfg, o.scene(args.scene), rows=range(y, y + 1), threads=cpu_quota())[0][y]
                      for y in rows])
     out["rows_vs_oracle"] = rows
     out["bitwise_vs_oracle"] = bool(np.array_equal(got[rows].view(np.uint32),
                                                    want.view(np.uint32)))
     if world > 1:
-        # the same accumulation chunk as the ranks used: then the frames are equal bit for bit
+        # the same chunk partition as the ranks used: then the frames are equal bit for bit
         ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
                                  max_depth=args.depth, device=device, kernel_variant=args.variant,
-                                 accumulate_chunk=st["accumulate_chunk"])
+                                 accumulate_chunk=st["accumulate_chunk"],
+                                 accumulate_tail=st["accumulate_tail"] or -1,
+                                 accumulate_tail_chunk=st["accumulate_tail_chunk"])
         with vc.Renderer(ref_desc, args.scene) as ref:
             ref.draw_next_frame()
             one = ref.read_framebuffer()
@@ -332,6 +334,7 @@ def main():
                        "parallelism": f"tiles8x8-diagonal-x{world}",
                        "gather": gather,
                        "accumulate_chunk": st["accumulate_chunk"],
+                       "accumulate_tail": [st["accumulate_tail"], st["accumulate_tail_chunk"]],
                        "kernel_variant": st["kernel_variant"],
                        "grid_blocks": st["grid_blocks"]},
             # fp32 VALU-bound (no MFMA). achieved = the fp32 work the timed

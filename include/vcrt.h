@@ -109,6 +109,13 @@ typedef struct vcrt_render_desc {
                             image as one render with (f+1)*spp samples and chunk boundaries at
                             every frame; RENDER_ITERATION, Common.hpp:25, was never wired up). */
     const char* code_object_path; /* NULL = vcrt_tracer.hsaco next to libvcrt.so, then embedded */
+    int32_t accumulate_tail;      /* the last accumulate_tail samples of every pixel (of every
+                                     progressive frame) in chunks of accumulate_tail_chunk, handed
+                                     out after all the other work items, so that the items still
+                                     running when the queue drains are short. 0 = the rule
+                                     (vcrt_work_tail), -1 = none. Part of the chunk partition: the
+                                     image depends on it as on accumulate_chunk. */
+    int32_t accumulate_tail_chunk; /* samples per tail item; 0 = the rule */
 } vcrt_render_desc;
 
 typedef struct vcrt_stats {
@@ -140,6 +147,8 @@ typedef struct vcrt_stats {
                            the camera fast trace with its shading; [24..31] camera fast
                            trace entries, its lanes, live lanes, listed-group loop trips and
                            lane sum, root loop trips and lane sum; main-scan hit lanes */
+    int32_t accumulate_tail;       /* tail samples per pixel in effect (0: none) */
+    int32_t accumulate_tail_chunk; /* samples per tail item in effect */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
@@ -150,6 +159,12 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc);
 /* Samples per work item (the accumulation chunk) that vcrt_begin(desc) uses; host only, no
  * GPU. Negative VkResult for an invalid desc. */
 int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
+/* Tail samples per pixel that vcrt_begin(desc) uses (0: none) and, in *tail_chunk, the samples
+ * per tail item; host only. The rule: about six head items per lane of the persistent grid,
+ * T = 6 * chunk * 327680 / (64 * the largest rank's tiles) rounded to a power of two, in items
+ * of max(4, chunk / 8) samples; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel.
+ * Negative VkResult for an invalid desc. */
+int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
  * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final
  * scene at 1080p, ~0.4 s for 4100 spheres at 4K). vcrt_begin sets the final scene. */

@@ -339,14 +339,25 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
     const int chunk =
         (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block) ? block
                                                                         : cfg->accumulate_chunk;
-    const int single = cfg->frame_spp <= 0 && chunk >= cfg->spp;
+    /* the tail: the last `tail` samples of each frame in chunks of tail_chunk */
+    const int tail = (cfg->accumulate_tail > 0 && cfg->accumulate_tail < block &&
+                      cfg->accumulate_tail_chunk > 0)
+                         ? cfg->accumulate_tail
+                         : 0;
+    const int single = cfg->frame_spp <= 0 && chunk >= cfg->spp && tail == 0;
     double sum[3] = {0.0, 0.0, 0.0};
     v3 part = V(0.0f, 0.0f, 0.0f);
     for (int c0 = 0; c0 < cfg->spp;) {
         part = V(0.0f, 0.0f, 0.0f);
-        const int block_end = (c0 / block + 1) * block;
-        int c1 = c0 + chunk < block_end ? c0 + chunk : block_end;
-        if (c1 > cfg->spp) c1 = cfg->spp;
+        int block_end = (c0 / block + 1) * block;
+        if (block_end > cfg->spp) block_end = cfg->spp;
+        const int tail_start = block_end - tail;
+        int c1;
+        if (c0 < tail_start)
+            c1 = c0 + chunk < tail_start ? c0 + chunk : tail_start;
+        else
+            c1 = c0 + cfg->accumulate_tail_chunk < block_end ? c0 + cfg->accumulate_tail_chunk
+                                                             : block_end;
         for (int i = c0; i < c1; i++) {
             float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
             v3 rs = vadd(vscale(jx, du), vscale(jy, dv));

@@ -39,9 +39,13 @@ typedef struct oracle_config {
      * every progressive frame of frame_spp samples (0: one frame). Each chunk is summed in fp32
      * in sample order. One chunk and no frames: sum / spp in fp32, the reference's sequential
      * sum (shader.comp:46-56) exactly. Otherwise the chunk sums are quantized to 2^-32 and
-     * added exactly, then divided in double: the GPU's order-independent combination. */
+     * added exactly, then divided in double: the GPU's order-independent combination.
+     * accumulate_tail > 0: the last accumulate_tail samples of every frame are cut into chunks
+     * of accumulate_tail_chunk instead (the head before them into chunks of accumulate_chunk). */
     int32_t accumulate_chunk;
     int32_t frame_spp;
+    int32_t accumulate_tail;
+    int32_t accumulate_tail_chunk;
 } oracle_config;
 
 /* Canonical math (see DESIGN.md "canonical math"). */

@@ -31,6 +31,8 @@ class OracleConfig(ctypes.Structure):
         ("vup", ctypes.c_float * 3), ("vfov", ctypes.c_float),
         ("accumulate_chunk", ctypes.c_int32),
         ("frame_spp", ctypes.c_int32),
+        ("accumulate_tail", ctypes.c_int32),
+        ("accumulate_tail_chunk", ctypes.c_int32),
     ]
 
 
@@ -81,10 +83,13 @@ class Oracle:
 
     @staticmethod
     def config(width, height, spp, max_depth, lookfrom=(13, 2, 3), lookat=(0, 0, 0),
-               vup=(0, 1, 0), vfov=20.0, chunk=0, frame_spp=0) -> OracleConfig:
+               vup=(0, 1, 0), vfov=20.0, chunk=0, frame_spp=0, tail=0,
+               tail_chunk=0) -> OracleConfig:
         c = OracleConfig()
         c.accumulate_chunk = chunk
         c.frame_spp = frame_spp
+        c.accumulate_tail = tail
+        c.accumulate_tail_chunk = tail_chunk
         c.width, c.height, c.spp, c.max_depth = width, height, spp, max_depth
         c.lookfrom[:] = [float(v) for v in lookfrom]
         c.lookat[:] = [float(v) for v in lookat]
@@ -96,6 +101,12 @@ class Oracle:
         out = np.zeros(15, dtype=np.float32)
         self.lib.oracle_camera(ctypes.byref(cfg), out.ctypes.data)
         return out
+
+    @staticmethod
+    def partition(stats: dict) -> dict:
+        """config() keywords for the chunk partition a render used (its stats)."""
+        return dict(chunk=stats["accumulate_chunk"], tail=stats["accumulate_tail"],
+                    tail_chunk=stats["accumulate_tail_chunk"])
 
     # ---- render ----
     def render(self, cfg: OracleConfig, spheres: np.ndarray, rows=None, threads: int = 0):

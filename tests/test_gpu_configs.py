@@ -73,7 +73,7 @@ def test_small_configs_whole_frame(oracle, name):
     scene, w, h, spp, depth = CONFIGS[name]
     got, st = render_full(name)
     frame_properties(got, st, name)
-    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"]),
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
                                oracle.scene(scene))
     check_subset(got, want, name)
     assert st["segments"] == segs
@@ -89,7 +89,7 @@ def test_final_scene_configs_row_subset(oracle, name):
     rows = range(67, h, 135)  # 8 rows: sky, the sphere field, the ground
     sel = list(rows)
     assert len(sel) == 8
-    cfg = oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"])
+    cfg = oracle.config(w, h, spp, depth, **oracle.partition(st))
     want, _ = oracle.render(cfg, oracle.scene(scene), rows=rows)
     check_subset(got[sel], want[sel], f"{name} rows {sel}")
     seq, _ = oracle.render(oracle.config(w, h, spp, depth), oracle.scene(scene), rows=rows)
@@ -98,7 +98,7 @@ def test_final_scene_configs_row_subset(oracle, name):
     assert got[sel][..., 2].max() > 0.9 and got[sel][..., 0].min() < 0.2
 
 
-def test_c4_sharded_eight_ways_equals_one_gpu():
+def test_c4_sharded_eight_ways_equals_one_gpu(oracle):
     """C4's 8-GPU decomposition rendered rank by rank on one GPU: every rank's tiles, gathered
     and re-interleaved by vcrt_assemble, give the 1-GPU frame with the same accumulation chunk
     bit for bit (chunk sums are combined exactly, in whatever order the ranks finish them)."""
@@ -106,9 +106,13 @@ def test_c4_sharded_eight_ways_equals_one_gpu():
     from vulkancomputeraytracing_amd import distributed as D
     scene, w, h, spp, depth = CONFIGS["c4"]
     world = 8
-    k8 = vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
-                                              world_size=world))
-    full, st1 = render_full("c4", accumulate_chunk=k8)  # the 8-way default chunk
+    d8 = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
+    k8 = vc.renderer.work_chunk(d8)
+    t8, kt8 = vc.renderer.work_tail(d8)
+    assert (k8, t8, kt8) == (16, 128, 4)
+    # the 8-way default partition (head chunk and tail) on one GPU
+    full, st1 = render_full("c4", accumulate_chunk=k8, accumulate_tail=t8,
+                            accumulate_tail_chunk=kt8)
     pad = D.tiles_per_rank(w, h, world)
     gathered = torch.zeros((world * pad * 64, 4), dtype=torch.float32, device="cuda:0")
     segs = 0
@@ -116,7 +120,7 @@ def test_c4_sharded_eight_ways_equals_one_gpu():
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, rank=rank, world_size=world)  # default chunk: k8
         with vc.Renderer(desc, scene) as r:
-            assert r.stats()["accumulate_chunk"] == st1["accumulate_chunk"]
+            assert oracle.partition(r.stats()) == oracle.partition(st1)
             r.set_framebuffer_device(gathered[rank * pad * 64:].data_ptr(), pad * 64 * 16)
             r.draw_next_frame()
             segs += r.stats()["segments"]
@@ -137,7 +141,7 @@ def test_c5_stress_pixel_grid(oracle):
     xs = np.linspace(17, w - 23, 8).astype(int)
     ys = np.linspace(31, h - 11, 8).astype(int)
     xy = [(int(x), int(y)) for y in ys for x in xs]
-    cfg = oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"])
+    cfg = oracle.config(w, h, spp, depth, **oracle.partition(st))
     want, _ = oracle.render_pixels(cfg, oracle.scene(scene), xy)
     sub = np.stack([got[y, x] for x, y in xy])
     check_subset(sub, want, "c5 8x8 pixel grid")

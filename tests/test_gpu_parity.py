@@ -30,10 +30,13 @@ def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0,
         return r.read_framebuffer(), r.stats()
 
 
-def chunk_of(w, h, spp, chunk=0):
-    """The accumulation chunk the renderer uses (C ABI vcrt_work_chunk, no re-implementation)."""
-    return vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
-                                                accumulate_chunk=chunk))
+def chunk_of(w, h, spp, chunk=0, world=1, tail=0, tail_chunk=0):
+    """The chunk partition the renderer uses, as oracle.config() keywords (C ABI vcrt_work_chunk
+    and vcrt_work_tail, no re-implementation)."""
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, accumulate_chunk=chunk,
+                         world_size=world, accumulate_tail=tail, accumulate_tail_chunk=tail_chunk)
+    t, kt = vc.renderer.work_tail(desc)
+    return dict(chunk=vc.renderer.work_chunk(desc), tail=t, tail_chunk=kt)
 
 
 def bits(a):
@@ -75,9 +78,9 @@ def expected_variant(variant, nspheres):
 def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     got, st = gpu_render(scene, w, h, spp, depth, variant)
     # default work split: the oracle sums in the same order (chunks of accumulate_chunk)
-    assert st["accumulate_chunk"] == chunk_of(w, h, spp)
+    assert oracle.partition(st) == chunk_of(w, h, spp)
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth,
-                                                  chunk=st["accumulate_chunk"]),
+                                                  **oracle.partition(st)),
                                     oracle.scene(scene))
     assert got.shape == want.shape
     assert_bitwise(got, want, f"{scene} {w}x{h} spp{spp} d{depth} v{variant}")
@@ -94,9 +97,9 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
 ])
 def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, variant):
     k = chunk_of(w, h, spp, chunk)
-    want, want_segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
     got, st = gpu_render(scene, w, h, spp, depth, variant, chunk=chunk)
-    assert st["accumulate_chunk"] == k
+    assert oracle.partition(st) == k
     assert_bitwise(got, want, f"{scene} spp{spp} chunk{k}")
     assert st["segments"] == want_segs
     # the chunked order stays within the north_star tolerance of the sequential order
@@ -104,6 +107,57 @@ def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth,
     rms = np.sqrt(((got.astype(np.float64) - seq) ** 2).mean(axis=(0, 1)))
     assert np.all(rms <= RMS_TOL), rms
     assert np.all(rms <= 1e-6), rms  # in practice a few ulps
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,tail,tail_chunk", [
+    ("final", 64, 36, 40, 10, 8, 12, 5),   # head 28 = 8+8+8+4, tail 12 = 5+5+2
+    ("three", 72, 40, 33, 8, 16, 9, 1),    # a tail of single samples
+    ("final", 40, 24, 20, 10, 16, 6, 4),   # the head one chunk of 14
+])
+def test_tail_partition_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, tail,
+                                          tail_chunk, variant):
+    """The tail of the chunk partition (the last samples of every pixel in their own items,
+    handed out after the head): the oracle's partition, bit for bit."""
+    k = chunk_of(w, h, spp, chunk, tail=tail, tail_chunk=tail_chunk)
+    assert (k["tail"], k["tail_chunk"]) == (tail, tail_chunk)
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         kernel_variant=variant, accumulate_chunk=chunk, accumulate_tail=tail,
+                         accumulate_tail_chunk=tail_chunk)
+    with vc.Renderer(desc, scene) as r:
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    assert oracle.partition(st) == k
+    assert_bitwise(got, want, f"{scene} spp{spp} {k}")
+    assert st["segments"] == want_segs
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_tail_partition_progressive_and_sharded(oracle, world):
+    """Progressive frames with a tail in each frame, rendered in `world` shards: every rank's
+    pixels equal the oracle's at every frame."""
+    w, h, spp, depth, frames = 56, 32, 10, 10, 2
+    part = dict(chunk=3, tail=4, tail_chunk=2)
+    m = vc.tile_pixel_map(w, h, world)
+    sc = oracle.scene("final")
+    wants = [oracle.render(oracle.config(w, h, (f + 1) * spp, depth, frame_spp=spp, **part),
+                           sc)[0] for f in range(frames)]
+    for rank in range(world):
+        desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
+                             device=0, rank=rank, world_size=world, progressive=True,
+                             accumulate_chunk=3, accumulate_tail=4, accumulate_tail_chunk=2)
+        mine = m[..., 0] == rank
+        with vc.Renderer(desc, "final") as r:
+            assert oracle.partition(r.stats()) == part
+            for f in range(frames):
+                r.draw_next_frame()
+                got = r.read_framebuffer()
+                if world > 1:
+                    got = got.reshape(-1, 4)[m[..., 1][mine]]
+                    assert_bitwise(got, wants[f][mine], f"rank {rank}/{world} frame {f}")
+                else:
+                    assert_bitwise(got, wants[f], f"frame {f}")
 
 
 def test_golden_oracle_images():
@@ -134,7 +188,7 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
     monkeypatch.setenv("VCRT_CULL_LANE_TABLES", tables)
     w, h, spp, depth = 40, 24, 3, 12
     k = chunk_of(w, h, spp, 0)
-    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k), oracle.scene(scene))
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
     got, st = gpu_render(scene, w, h, spp, depth, vc.KERNEL_CULL_LANE)
     assert st["kernel_variant"] == vc.KERNEL_CULL_LANE
     assert_bitwise(got, want, f"{scene} lane tables={tables}")
@@ -199,7 +253,7 @@ def test_large_random_scene_all_variants(oracle, n):
     w, h, spp, depth = 40, 24, 2, 8
     cfg = dict(lookfrom=(-80, 10, 5), lookat=(0, 0, 0), vfov=50)
     k = chunk_of(w, h, spp, 0)
-    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **k, **cfg), sc)
     for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, kernel_variant=variant, **cfg)
@@ -219,7 +273,7 @@ def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
     assert len(sc) >= 16
     cfg = dict(lookfrom=(6, 2.5, 5), lookat=(0, 0.6, 0), vfov=45)
     k = chunk_of(w, h, spp, chunk)
-    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cfg), sc)
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **k, **cfg), sc)
     for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, kernel_variant=variant, accumulate_chunk=chunk, **cfg)
@@ -247,7 +301,7 @@ def test_camera_ray_lists_bitwise(oracle, cam):
     pl = S.primary_lists(sc, vc.RenderDesc(width=w, height=h, **cam))
     assert ((pl["info"] & 15) != 15).mean() > 0.3  # the lists are in use
     k = chunk_of(w, h, spp, 0)
-    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=k, **cam), sc)
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **k, **cam), sc)
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
                          **cam)
     with vc.Renderer(desc, "final") as r:
@@ -383,7 +437,7 @@ def test_full_size_rows_subset_rms(oracle, variant):
     w, h, spp, depth = 1920, 1080, 16, 10
     got, st = gpu_render("final", w, h, spp, depth, variant)
     rows = range(7, h, 90)
-    want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"]),
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
                             oracle.scene("final"), rows=rows)
     sel = list(rows)
     g, o = got[sel].astype(np.float64), want[sel].astype(np.float64)
@@ -417,7 +471,7 @@ def test_progressive_frames_bitwise(oracle, spp, chunk):
                          progressive=True, accumulate_chunk=chunk)
     scene = oracle.scene("final")
     with vc.Renderer(desc, "final") as r:
-        k = r.stats()["accumulate_chunk"]
+        k = oracle.partition(r.stats())
         outs = []
         for f in range(frames):
             r.draw_next_frame()
@@ -427,7 +481,7 @@ def test_progressive_frames_bitwise(oracle, spp, chunk):
         r.draw_next_frame()
         again = r.read_framebuffer()
     for f, got in enumerate(outs):
-        want, _ = oracle.render(oracle.config(w, h, (f + 1) * spp, depth, chunk=k,
+        want, _ = oracle.render(oracle.config(w, h, (f + 1) * spp, depth, **k,
                                               frame_spp=spp), scene)
         assert_bitwise(got, want, f"progressive frame {f}")
     assert_bitwise(again, outs[0], "after reset")
@@ -497,7 +551,7 @@ def test_rccl_comm_inside_libvcrt_world1(oracle):
             r.set_framebuffer_device(1 << 20, 1 << 30)
         r.draw_next_frame()
         got, st = r.read_framebuffer(), r.stats()
-    want, segs = oracle.render(oracle.config(w, h, spp, depth, chunk=st["accumulate_chunk"]),
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
                                oracle.scene("final"))
     assert_bitwise(got, want, "comm world 1")
     assert st["segments"] == segs
@@ -527,15 +581,14 @@ def test_sharded_camera_ray_lists_bitwise(oracle, world):
     from vulkancomputeraytracing_amd import scene as S
     w, h, spp, depth = 320, 180, 2, 10
     sc = S.builtin_scene("final")
-    k = vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
-                                             world_size=world))
-    want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=k), sc)
+    k = chunk_of(w, h, spp, world=world)
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, **k), sc)
     m = vc.tile_pixel_map(w, h, world)
     for rank in range(world):
         pl = S.primary_lists(sc, vc.RenderDesc(width=w, height=h, rank=rank, world_size=world))
         assert ((pl["info"] & 15) != 15).mean() > 0.5
         part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world)
-        assert st["accumulate_chunk"] == k  # every rank: the largest rank's default
+        assert oracle.partition(st) == k  # every rank: the largest rank's default
         mine = m[..., 0] == rank
         assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], f"rank {rank}/{world}")
 

@@ -184,6 +184,62 @@ def test_work_chunk_rule(w, h, spp):
                                                         world_size=world)) == want
 
 
+@pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (1, 1)])
+@pytest.mark.parametrize("spp", [1, 16, 64, 256, 1024, 4096])
+def test_work_tail_rule(w, h, spp):
+    """vcrt_work_tail (the tail of the chunk partition; host only): the same for every rank,
+    restated here -- T = 6 * K * 327680 / (64 * the largest rank's tiles) to the nearest power of
+    two, items of max(4, K / 8) samples, none when 4 T > spp or K >= spp -- and explicit values
+    (capped below spp) or -1 (none) taken as given."""
+    import math
+    for world in (1, 2, 3, 8):
+        parts = set()
+        for rank in range(world):
+            d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, rank=rank,
+                              world_size=world)
+            parts.add((vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d))
+        assert len(parts) == 1
+        k, t, kt = parts.pop()
+        slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
+        raw = 6 * 327680 * k / slots
+        want = 0
+        if k < spp and raw >= 1:
+            want = 1 << round(math.log2(raw))
+            if 4 * want > spp:
+                want = 0
+        assert t == want
+        assert kt == (min(max(4, k // 8), t) if t else 0)
+        d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world,
+                          accumulate_chunk=k, accumulate_tail=5, accumulate_tail_chunk=2)
+        t5 = vc.renderer.work_tail(d)
+        assert t5 == ((0, 0) if k >= spp else (min(5, spp - 1), min(2, min(5, spp - 1))))
+        d.accumulate_tail = -1
+        assert vc.renderer.work_tail(d) == (0, 0)
+    if (w, h, spp) == (1920, 1080, 1024):  # the bench config on 1/2/4/8 GPUs
+        for world, want in ((1, (64, 64, 8)), (2, (32, 64, 4)), (4, (16, 64, 4)),
+                            (8, (16, 128, 4))):
+            d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
+            assert (vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d) == want
+
+
+def test_oracle_tail_partition(oracle):
+    """The oracle's tail: a tail cut on the head's own chunk boundaries into chunks of the same
+    size is the same partition (same bits); another cut moves the image by rounding only."""
+    sc = oracle.scene("three")
+    w, h, spp, depth = 24, 14, 24, 6
+    plain, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=4), sc)
+    same, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=4, tail=8, tail_chunk=4), sc)
+    assert np.array_equal(plain.view(np.uint32), same.view(np.uint32))
+    other, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=4, tail=7, tail_chunk=3), sc)
+    assert not np.array_equal(plain.view(np.uint32), other.view(np.uint32))
+    assert np.abs(other - plain).max() < 1e-6
+    # progressive: the tail repeats in every frame of frame_spp samples
+    prog, _ = oracle.render(oracle.config(w, h, 2 * spp, depth, chunk=4, frame_spp=spp, tail=8,
+                                          tail_chunk=4), sc)
+    prog0, _ = oracle.render(oracle.config(w, h, 2 * spp, depth, chunk=4, frame_spp=spp), sc)
+    assert np.array_equal(prog.view(np.uint32), prog0.view(np.uint32))
+
+
 def test_work_chunk_rejects_invalid_desc():
     lib = N.lib()
     d = vc.RenderDesc(width=0, height=10, samples_per_pixel=4).to_c()

@@ -76,6 +76,8 @@ class vcrt_render_desc(ctypes.Structure):
         ("accumulate_chunk", ctypes.c_int32),
         ("progressive", ctypes.c_int32),
         ("code_object_path", ctypes.c_char_p),
+        ("accumulate_tail", ctypes.c_int32),
+        ("accumulate_tail_chunk", ctypes.c_int32),
     ]
 
 
@@ -102,6 +104,8 @@ class vcrt_stats(ctypes.Structure):
         ("bound_tests", ctypes.c_uint64),
         ("kernel", ctypes.c_char * 48),
         ("debug", ctypes.c_uint64 * 32),
+        ("accumulate_tail", ctypes.c_int32),
+        ("accumulate_tail_chunk", ctypes.c_int32),
     ]
 
 
@@ -114,6 +118,8 @@ SIGNATURES = {
     "vcrt_default_desc": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_begin": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_work_chunk": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
+    "vcrt_work_tail": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc),
+                                        ctypes.POINTER(ctypes.c_int32)]),
     "vcrt_set_scene": (ctypes.c_int32, [ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_draw_next_frame": (ctypes.c_int32, []),
     "vcrt_end": (ctypes.c_int32, []),

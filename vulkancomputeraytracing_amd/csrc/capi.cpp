@@ -83,6 +83,7 @@ struct RendererState {
     bool primary_lists = true;        // VCRT_PRIMARY_LISTS=0 turns them off
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
+    int32_t tail_start = 0, tail_chunk = 1, tail_nchunks = 0;  // TraceParams' tail
     uint32_t total_pixels = 0, total_items = 0;
     bool direct = false;  // one item per pixel, not progressive: lanes write pixels (kFlagDirect)
     double* d_accum = nullptr;  // [total_pixels][4] exact sums of the quantized chunk sums
@@ -163,6 +164,38 @@ int32_t work_chunk(const vcrt_render_desc& d) {
                           ? d.accumulate_chunk
                           : default_chunk(64ull * max_tiles, d.samples_per_pixel);
     return std::min(k, d.samples_per_pixel);
+}
+
+// The tail of the partition (vcrt.h vcrt_work_tail): the last T samples of every pixel in items
+// of KT samples, handed out after the head. An item started just before the queue drains runs to
+// its end while the rest of the chip idles, and its latency is K samples' worth of wave
+// iterations (~13 us each at full occupancy: up to ~2 ms at K = 16, ~8 ms at K = 64). The tail
+// keeps every lane busy with short items until the head's last items are done, so the head must
+// cover ~6 of its items per lane: T ~ 6 K L / P for the L = 327680 lanes of the persistent grid and
+// the P pixel slots of the largest rank. Measured at C4 (profiles/r02_tail_sweep.txt, kernel ms):
+// one GPU K = 64 128.2 -> 127.0 with T = 64, KT = 8; 8-way shards K = 16 18.0 -> 17.6 with
+// T = 128, KT = 4 (a head of K = 64 stays above 21 ms at N = 8 with any tail up to 384).
+constexpr uint64_t kTailLaneItems = 6ull * 327680ull;
+
+int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk) {
+    const int32_t spp = d.samples_per_pixel;
+    *tail_chunk = 1;
+    if (d.accumulate_tail < 0 || chunk >= spp) return 0;
+    int32_t t = 0, kt = d.accumulate_tail_chunk;
+    if (d.accumulate_tail > 0) {
+        t = std::min(d.accumulate_tail, spp - 1);
+    } else {
+        uint32_t max_tiles = 0;
+        for (int32_t rr = 0; rr < d.world_size; rr++)
+            max_tiles = std::max(max_tiles, tiles_for_rank(d.width, d.height, d.world_size, rr));
+        const double raw = static_cast<double>(kTailLaneItems) * chunk / (64.0 * max_tiles);
+        if (raw < 1.0) return 0;
+        t = 1 << static_cast<int>(std::lround(std::log2(raw)));  // nearest power of two
+        if (4 * static_cast<int64_t>(t) > spp) return 0;
+    }
+    if (kt <= 0) kt = std::max(4, chunk / 8);
+    *tail_chunk = std::min(kt, t);
+    return t;
 }
 
 // Jitter of sample indices base .. base+n-1 (shader.comp:48 depends only on the index).
@@ -321,6 +354,7 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (d.width > 65535 || d.height > 65535) return false;  // kernels pack y << 16 | x
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
+    if (d.accumulate_tail < -1 || d.accumulate_tail_chunk < 0) return false;
     if (d.progressive != 0 && d.progressive != 1) return false;
     if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL_FLAT) return false;
     return true;
@@ -415,6 +449,11 @@ int32_t vcrt_work_chunk(const vcrt_render_desc* desc) {
     return work_chunk(*desc);
 }
 
+int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk) {
+    if (!desc || !desc_valid(*desc) || !tail_chunk) return VCRT_ERROR_INITIALIZATION_FAILED;
+    return work_tail(*desc, work_chunk(*desc), tail_chunk);
+}
+
 vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (!desc || !desc_valid(*desc)) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (g.begun) vcrt_end();
@@ -505,12 +544,18 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     // combined exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks of them.
     g.total_pixels = g.local_tiles * 64u;  // local element slots incl. partial-tile padding
     g.chunk = work_chunk(g.desc);
-    g.nchunks = (spp + g.chunk - 1) / g.chunk;
-    if (g.nchunks > vcrt::kAccumMaxChunks) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
-    g.direct = g.nchunks == 1 && !g.desc.progressive;
     {
-        const uint64_t items =
-            static_cast<uint64_t>(g.total_pixels) * static_cast<uint64_t>(g.nchunks);
+        const int32_t t = work_tail(g.desc, g.chunk, &g.tail_chunk);
+        g.tail_start = spp - t;
+        g.tail_nchunks = t > 0 ? (t + g.tail_chunk - 1) / g.tail_chunk : 0;
+    }
+    g.nchunks = (g.tail_start + g.chunk - 1) / g.chunk;
+    if (g.nchunks + g.tail_nchunks > vcrt::kAccumMaxChunks)
+        return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
+    g.direct = g.nchunks == 1 && g.tail_nchunks == 0 && !g.desc.progressive;
+    {
+        const uint64_t items = static_cast<uint64_t>(g.total_pixels) *
+                               static_cast<uint64_t>(g.nchunks + g.tail_nchunks);
         if (items >= (uint64_t{1} << 31)) return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
         g.total_items = static_cast<uint32_t>(items);
     }
@@ -546,6 +591,8 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         return fail(r);
     g.stats.local_tiles = static_cast<int32_t>(g.local_tiles);
     g.stats.accumulate_chunk = g.chunk;
+    g.stats.accumulate_tail = spp - g.tail_start;
+    g.stats.accumulate_tail_chunk = g.tail_nchunks > 0 ? g.tail_chunk : 0;
     return VCRT_SUCCESS;
 }
 
@@ -696,7 +743,7 @@ vcrt_result vcrt_draw_next_frame(void) {
     // progressive frames add chunks to the pixels' exact sums: at most kAccumMaxChunks in all
     if (g.desc.progressive &&
         (g.accumulated / static_cast<uint64_t>(g.desc.samples_per_pixel) + 1) *
-                static_cast<uint64_t>(g.nchunks) >
+                static_cast<uint64_t>(g.nchunks + g.tail_nchunks) >
             static_cast<uint64_t>(vcrt::kAccumMaxChunks))
         return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
     if (g.desc.progressive && g.accumulated > 0) {
@@ -743,6 +790,10 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.total_items = g.total_items;
         p.chunk = g.chunk;
         p.nchunks = g.nchunks;
+        p.tail_start = g.tail_start;
+        p.tail_chunk = g.tail_chunk;
+        p.tail_nchunks = g.tail_nchunks;
+        p.blocks_head = g.local_tiles * static_cast<uint32_t>(g.nchunks);
         p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
                   (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
                   (g.direct ? vcrt::kFlagDirect : 0u);

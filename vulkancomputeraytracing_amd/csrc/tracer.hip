@@ -1273,6 +1273,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     // the wave's current block of items (wave-uniform); 64 = exhausted, fetch a new one
     const uint32_t total_blocks = p.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
+    uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
+    bool blk_tail = false;
 
     // Shades a traced segment (textures.glsl, or the sky of functions.glsl:85-89) and advances
     // the lane's path: accumulate and start the next sample's camera ray (returns true), or
@@ -1420,10 +1422,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     if (need) done = true;
                     break;
                 }
-                if (reverse) b = total_blocks - 1u - b;
-                // block b = (local tile lt, chunk): wave-uniform tile origin and sample range
-                blk_lt = b / nchunks;
-                blk_chunk = b - blk_lt * nchunks;
+                // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
+                // tile origin and sample range; reversed within each part
+                blk_tail = b >= p.blocks_head;
+                if (blk_tail) b -= p.blocks_head;
+                if (reverse) b = (blk_tail ? total_blocks - p.blocks_head : p.blocks_head) - 1u - b;
+                blk_nch = blk_tail ? (uint32_t)p.tail_nchunks : nchunks;
+                blk_lt = b / blk_nch;
+                blk_chunk = b - blk_lt * blk_nch;
                 tile_of(blk_lt, (uint32_t)p.rank, (uint32_t)p.world, p.tiles_x, &blk_tx, &blk_ty);
                 blk_next = 0u;
             }
@@ -1433,9 +1439,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 uint32_t slot = blk_next + mine, ch = blk_chunk;
                 if (chunk_minor) {  // item 64 j + slot of the tile = (pixel, chunk), chunk-minor
                     const uint32_t i = 64u * blk_chunk + slot;
-                    slot = i / nchunks;
-                    ch = i - slot * nchunks;
+                    slot = i / blk_nch;
+                    ch = i - slot * blk_nch;
                 }
+                if (blk_tail) ch |= 0x10000u;  // chunk ch of the tail
                 const uint32_t px = 8u * blk_tx + (slot & 7u), py = 8u * blk_ty + (slot >> 3);
                 if (px < (uint32_t)p.width && py < (uint32_t)p.height) {  // edge tiles: skip
                     got = true;
@@ -1455,8 +1462,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             pxy = (g_py << 16) | g_px;
             // shader.comp:43  pixel00 + x*delta_u + y*delta_v
             acc = mk(0.f, 0.f, 0.f);
-            sample = (int)(g_chunk * (uint32_t)p.chunk);
-            sample_end = min(sample + p.chunk, p.spp);
+            const bool tail = g_chunk >= 0x10000u;
+            const int k = tail ? p.tail_chunk : p.chunk;
+            sample = (tail ? p.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
+            sample_end = min(sample + k, tail ? p.spp : p.tail_start);
             // first camera ray of the chunk, shader.comp:48-52
             const float2 jt = p.jitter[sample];
             const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));

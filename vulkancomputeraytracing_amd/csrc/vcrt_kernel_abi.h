@@ -65,9 +65,14 @@ struct TraceParams {
     int32_t rank, world;
     uint32_t tiles_x;      // ceil(width / 8)
     uint32_t local_tiles;  // tiles owned by this rank
-    uint32_t total_items;  // local_tiles * 64 * nchunks
-    int32_t chunk;         // samples per work item (<= kAccumMaxChunk)
-    int32_t nchunks;       // ceil(spp / chunk)
+    uint32_t total_items;  // local_tiles * 64 * (nchunks + tail_nchunks)
+    int32_t chunk;         // samples per work item (<= kAccumMaxChunk) of the head
+    int32_t nchunks;       // ceil(tail_start / chunk)
+    // The tail: samples tail_start .. spp-1 of every pixel in chunks of tail_chunk (tail_nchunks
+    // of them), handed out after all head blocks (the first blocks_head = local_tiles *
+    // nchunks). No tail: tail_start = spp, tail_nchunks = 0.
+    int32_t tail_start, tail_chunk, tail_nchunks;
+    uint32_t blocks_head;
     uint32_t flags;        // kFlag*
     float spp_total;       // kFlagDirect: the divisor (samples per pixel)
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz

@@ -35,6 +35,8 @@ class RenderDesc:
     accumulate_chunk: int = 0       # 0 = from the frame (work_chunk); >= spp: sequential order
     progressive: bool = False       # frame f continues the sample sequence; average of all frames
     code_object_path: str | None = None
+    accumulate_tail: int = 0        # tail samples per pixel: 0 = the rule (work_tail), -1 = none
+    accumulate_tail_chunk: int = 0  # samples per tail item; 0 = the rule
     _path_keepalive: bytes | None = field(default=None, repr=False)
 
     def to_c(self) -> N.vcrt_render_desc:
@@ -52,6 +54,8 @@ class RenderDesc:
         d.blocks_per_cu = self.blocks_per_cu
         d.accumulate_chunk = self.accumulate_chunk
         d.progressive = 1 if self.progressive else 0
+        d.accumulate_tail = self.accumulate_tail
+        d.accumulate_tail_chunk = self.accumulate_tail_chunk
         if self.code_object_path:
             self._path_keepalive = self.code_object_path.encode()
             d.code_object_path = self._path_keepalive
@@ -62,6 +66,16 @@ def work_chunk(desc: RenderDesc) -> int:
     """Samples per work item (the accumulation chunk) the renderer uses for `desc`, from the
     C ABI (vcrt_work_chunk: host only, no GPU). The oracle's `chunk` for the same image."""
     return N.check_count("vcrt_work_chunk", N.lib().vcrt_work_chunk(ctypes.byref(desc.to_c())))
+
+
+def work_tail(desc: RenderDesc) -> tuple[int, int]:
+    """(tail samples per pixel, samples per tail item) the renderer uses for `desc`, from the
+    C ABI (vcrt_work_tail: host only, no GPU); (0, 0) when there is no tail. With work_chunk,
+    the oracle's chunk partition for the same image."""
+    kt = ctypes.c_int32(0)
+    t = N.check_count("vcrt_work_tail", N.lib().vcrt_work_tail(ctypes.byref(desc.to_c()),
+                                                                ctypes.byref(kt)))
+    return (t, kt.value) if t > 0 else (0, 0)
 
 
 def tiles_for_rank(width: int, height: int, world: int, rank: int) -> list[int]:
