@@ -47,7 +47,11 @@ def gather_tiles(local, tiles_pad: int, group=None, dst: int = 0):
         full = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
                            dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(full, local, group=group)
-        return full if rank == dst else None
+        out = full if rank == dst else None
+    if local.is_cuda:
+        # every rank: the collective is ordered on torch's current stream only, and the
+        # renderer's next frame (on its own stream) rewrites `local`; wait until it has been sent
+        torch.cuda.current_stream(local.device).synchronize()
     return out
 
 
