@@ -99,10 +99,10 @@ typedef struct vcrt_render_desc {
                                  within a chunk; one chunk (>= samples_per_pixel) is divided in
                                  fp32, the reference's sequential sum (shader.comp:46-56)
                                  exactly; several chunk sums are quantized to 2^-32 and added
-                                 exactly, so the image depends on the chunk only, not on the
-                                 schedule: a sharded frame equals a one-GPU render with the same
-                                 chunk. At most 512 chunks per pixel (progressive frames
-                                 included). */
+                                 exactly, so the image depends on the chunk partition (this
+                                 and the tail below) only, not on the schedule: a sharded frame
+                                 equals a one-GPU render with the same partition. At most 512
+                                 chunks per pixel (tail and progressive frames included). */
     int32_t progressive; /* 0: every DrawNextFrame re-renders samples 0..spp-1 (the reference,
                             Linux.cpp:362-366). 1: frame f renders samples f*spp..(f+1)*spp-1 and
                             the framebuffer holds the average of all frames so far (the same
