@@ -93,7 +93,7 @@ typedef struct vcrt_render_desc {
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
     int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 16 while the
-                                 largest rank's share has < 2^25 - 2^22 items, at least
+                                 largest rank's share has < 2^24 - 2^21 items, at least
                                  spp / 512:
                                  vcrt_work_chunk). A pixel's samples are summed in fp32 in order
                                  within a chunk; one chunk (>= samples_per_pixel) is divided in

@@ -10,7 +10,7 @@ REPS=${REPS:-2}
 for rep in $(seq 1 $REPS); do
   for c in $TAILS; do
     IFS=: read -r k t kt <<< "$c"
-    timeout -k 10 300 python tools/shard_sweep.py --chunk $k --tail $t --tail-chunk $kt \
+    timeout -k 10 300 python tools/shard_sweep.py --spp ${SPP:-1024} --chunk $k --tail $t --tail-chunk $kt \
       --worlds $WORLDS > gpurun_out/tail_${k}_${t}_${kt}_r$rep.json 2>/dev/null || exit 1
     echo "rep $rep $c done"
   done

@@ -120,17 +120,18 @@ RendererState g;
     } while (0)
 
 // Samples per work item when the caller leaves it to us: 64, halved (down to 16) while the
-// largest rank's share of the frame would be fewer than kChunkItems = 2^25 - 2^22 items (~90 per
-// lane of the persistent grid, ~330k lanes on MI355X), so the drain at the end of the queue
-// stays short; at least spp / 512 (at most kAccumMaxChunks chunks per pixel). Smaller items cost
-// more than they save in balance: every item start and end (slot fetch, pixel set-up, three f64
-// atomics whose completion later loads wait for) is paid by the whole wave. Measured at round 2
-// (profiles/r02_chunk_sweep.txt; per-rank kernel ms at K = 8 / 16 / 32 / 64): C4 on
-// one GPU 153.6 / 144.4 / 141.2 / 139.7 -> 64; its 2-way shards 76.7 / 72.7 / 71.5 / 73.4 -> 32;
-// 4-way 38.7 / 36.9 / 37.6 / 41.2 -> 16; 8-way 19.8 / 19.5 / 20.9 / 25.5 -> 16; C3 36.8 / 37.5 /
-// 41.4 at K = 16 / 32 / 64 -> 16. All ranks of a frame use the same K (the largest rank's share
-// decides), so a sharded frame equals a one-GPU render with that K bit for bit.
-constexpr uint64_t kChunkItems = (uint64_t{1} << 25) - (uint64_t{1} << 22);
+// largest rank's share of the frame would be fewer than kChunkItems = 2^24 - 2^21 items (~45 per
+// lane of the persistent grid, ~330k lanes on MI355X); at least spp / 512 (at most
+// kAccumMaxChunks chunks per pixel). Smaller items cost more than they save in balance: every
+// item start and end (slot fetch, pixel set-up, three f64 atomics whose completion later loads
+// wait for) is paid by the whole wave, and the tail of the partition (work_tail) now absorbs the
+// drain that small items used to shorten. Measured at round 2 with the tail
+// (profiles/r02_tail_sweep.txt, kernel ms per rank at the C4 workload): one GPU K = 64 127.0 /
+// K = 32 129.3 -> 64; 2-way shards 64.3 / 65.2 -> 64; 4-way K = 32 33.4 / K = 16 33.9 -> 32;
+// 8-way K = 16 17.6 / K = 32 17.7-18.1 -> 16; C3 (256 spp) K = 32 33.55 / K = 16 33.80 -> 32.
+// All ranks of a frame use the same K (the largest rank's share decides), so a sharded frame
+// equals a one-GPU render with that partition bit for bit.
+constexpr uint64_t kChunkItems = (uint64_t{1} << 24) - (uint64_t{1} << 21);
 
 int32_t default_chunk(uint64_t rank_slots, int32_t spp) {
     int32_t k = kDefaultChunk;
