@@ -13,7 +13,18 @@ if [ -n "$REV" ]; then
   INC=$T/include
 fi
 mkdir -p "$ROOT/ab_objs"
-/opt/rocm/bin/hipcc --genco --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math \
-  -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics \
-  $EXTRA -I"$INC" -I"$SRC" "$SRC/tracer.hip" -o "$ROOT/ab_objs/$NAME.hsaco"
+# the Makefile's recipe: two code-generation parts (VCRT_PART), linked into one code object
+L=/opt/rocm/lib/llvm/bin
+W=$(mktemp -d)
+for part in 1 2; do
+  /opt/rocm/bin/hipcc --cuda-device-only -emit-llvm -c --offload-arch=gfx950 -O3 -std=c++17 \
+    -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt \
+    -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics $EXTRA -I"$INC" -I"$SRC" \
+    -I/opt/rocm/include -DVCRT_PART=$part "$SRC/tracer.hip" -o "$W/p$part.bc"
+done
+$L/llc -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -filetype=obj -amdgpu-use-amdgpu-trackers=1 \
+  $LLC_EXTRA "$W/p1.bc" -o "$W/p1.o"
+$L/llc -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -filetype=obj $LLC_EXTRA "$W/p2.bc" -o "$W/p2.o"
+$L/ld.lld -shared "$W/p1.o" "$W/p2.o" -o "$ROOT/ab_objs/$NAME.hsaco"
+rm -rf "$W"
 echo "$ROOT/ab_objs/$NAME.hsaco"

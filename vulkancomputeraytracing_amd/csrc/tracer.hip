@@ -1711,6 +1711,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
 
 }  // namespace
 
+#ifndef VCRT_FLAT_WAVES
+#define VCRT_FLAT_WAVES 5  // waves per SIMD the flat scans are compiled for (LDS allows 5)
+#endif
+
+// VCRT_PART selects the kernels of one code-generation unit (Makefile: the global-table flat
+// kernels are compiled apart, with the default scheduler settings); unset: every kernel.
+#if !defined(VCRT_PART) || VCRT_PART == 1
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_lds(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_geom[];
     trace_impl<true, false>(p, lds_geom);
@@ -1746,9 +1753,6 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats
 
 // Per-lane scan with the exact phase flattened over the wave (exact_flat): LDS tables plus
 // 3.5 KB of scratch per wave.
-#ifndef VCRT_FLAT_WAVES
-#define VCRT_FLAT_WAVES 5  // waves per SIMD the flat scan is compiled for (LDS allows 5)
-#endif
 extern "C" __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
@@ -1760,6 +1764,9 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_stats(Tra
     trace_impl<false, true, 4>(p, lds_tab);
 }
 
+#endif
+
+#if !defined(VCRT_PART) || VCRT_PART == 2
 // The flat scan for tables too large for LDS beside its stacks (the stress scene): tables in
 // global memory (L2-resident), 32-bit stack entries (any group count), stacks alone in LDS.
 extern "C" __global__ __launch_bounds__(256)
@@ -1773,6 +1780,9 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_global_st
     trace_impl<false, true, 5>(p, lds_tab);
 }
 
+#endif
+
+#if !defined(VCRT_PART) || VCRT_PART == 1
 // The same with 1024-thread workgroups: one table copy serves 16 waves, so tables of up to
 // 160 KB (the whole LDS of a CU; 4100 spheres take 108 KB) still live in LDS.
 extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_lane_lds_wide(TraceParams p) {
@@ -1898,3 +1908,4 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_fill(FillParams p) {
          i += gridDim.x * blockDim.x)
         p.out[i] = p.value;
 }
+#endif
