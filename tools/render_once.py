@@ -24,12 +24,15 @@ def main():
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--rank", type=int, default=0)
     p.add_argument("--world", type=int, default=1)
+    p.add_argument("--tail", type=int, default=0, help="accumulate_tail (0 = rule, -1 = none)")
+    p.add_argument("--tail-chunk", type=int, default=0)
     a = p.parse_args()
     desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
                          max_depth=a.depth, kernel_variant=a.variant,
                          blocks_per_cu=a.blocks_per_cu, device=0,
                          code_object_path=a.code_object, accumulate_chunk=a.chunk,
-                         rank=a.rank, world_size=a.world)
+                         rank=a.rank, world_size=a.world, accumulate_tail=a.tail,
+                         accumulate_tail_chunk=a.tail_chunk)
     with vc.Renderer(desc, a.scene) as r:
         out = []
         for _ in range(a.frames):
