@@ -22,7 +22,7 @@ for part in 1 2; do
     -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics $EXTRA -I"$INC" -I"$SRC" \
     -I/opt/rocm/include -DVCRT_PART=$part "$SRC/tracer.hip" -o "$W/p$part.bc"
 done
-$L/llc -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -filetype=obj -amdgpu-use-amdgpu-trackers=1 \
+$L/llc -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -filetype=obj -amdgpu-use-amdgpu-trackers=1 $LLC_EXTRA1 \
   $LLC_EXTRA "$W/p1.bc" -o "$W/p1.o"
 $L/llc -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 -O3 -filetype=obj $LLC_EXTRA $LLC_EXTRA2 "$W/p2.bc" -o "$W/p2.o"
 $L/ld.lld -shared "$W/p1.o" "$W/p2.o" -o "$ROOT/ab_objs/$NAME.hsaco"
