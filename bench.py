@@ -22,6 +22,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3        # MI355X FP32 vector (packed FMA), MI355X_MICROARCH.md chip table
+PEAK_FP32_NONFMA_TFLOPS = 78.65  # the same issue rate without FMA (1 flop per lane-op of a packed
+                                 # add/mul): the ceiling of the exact sphere test, which parity
+                                 # keeps free of contraction
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
 FLOPS_PER_BOUND_TEST = 26       # tracer.hip box_gap, per box: 6 fma 12, per-axis min/max 6,
                                 # tnear/tfar 4, gap sub + add + fma 4
@@ -271,14 +274,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = r.stats()
-    validated = None
-    if args.validate and rank == 0:
-        if frame is not None:
-            got = frame.cpu().numpy()
-        else:
-            got = r.read_framebuffer()
-        validated = validate(args, got, st, device, world)
+    got = None
+    if args.validate and rank == 0:  # a host copy, before the renderer closes
+        got = frame.cpu().numpy() if frame is not None else r.read_framebuffer()
+    # close before validate(): libvcrt keeps one renderer per process, and validate() opens
+    # its own (a second vcrt_begin would end this one, communicator included)
     r.close()
+    validated = validate(args, got, st, device, world) if got is not None else None
 
     if rank == 0:
         samples = args.width * args.height * args.spp * args.steps
@@ -345,6 +347,8 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "peak_nonfma": PEAK_FP32_NONFMA_TFLOPS,
+                         "frac_nonfma": round(achieved / PEAK_FP32_NONFMA_TFLOPS, 4),
                          "traffic": prof.get("hbm_bytes_per_launch"),
                          "kernel": kernel, "kernel_ms": round(k_ms, 3),
                          "numerator": "issued fp32 work per launch: wave-level exact group "

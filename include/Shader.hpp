@@ -19,7 +19,8 @@ typedef struct VkPipelineShaderStageCreateInfo {
     int32_t sType;
     VkShaderStageFlagBits stage;
     void* module;      /* hipModule_t */
-    const char* pName; /* primary kernel symbol */
+    const char* pName; /* the tracer entry point: named by the renderer for its scene and desc
+                          (capi.cpp select_kernel); NULL out of CreateShaderStageFromFile */
 } VkPipelineShaderStageCreateInfo;
 
 // Load & bind. filename == nullptr selects the code object embedded in libvcrt.so.

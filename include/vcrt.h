@@ -163,6 +163,8 @@ int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
  * per tail item; host only. The rule: about six head items per lane of the persistent grid,
  * T = 6 * chunk * 327680 / (64 * the largest rank's tiles) rounded to a power of two, in items
  * of max(4, chunk / 8) samples; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel.
+ * Head and tail together take at most 512 chunks per pixel: a rule-made tail item grows until
+ * the tail fits beside the head (or the tail is dropped when the head leaves no room).
  * Negative VkResult for an invalid desc. */
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for

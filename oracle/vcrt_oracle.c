@@ -339,11 +339,15 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
     const int chunk =
         (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block) ? block
                                                                         : cfg->accumulate_chunk;
-    /* the tail: the last `tail` samples of each frame in chunks of tail_chunk */
-    const int tail = (cfg->accumulate_tail > 0 && cfg->accumulate_tail < block &&
-                      cfg->accumulate_tail_chunk > 0)
-                         ? cfg->accumulate_tail
+    /* the tail: the last `tail` samples of each frame in chunks of tail_chunk, clamped as the
+     * product's work_tail clamps explicit values (capi.cpp): at most block - 1 samples, items of
+     * at most `tail` samples, none when one chunk covers the frame (no rule here: a tail chunk
+     * <= 0 means no tail) */
+    const int tail = (cfg->accumulate_tail > 0 && chunk < block && cfg->accumulate_tail_chunk > 0)
+                         ? (cfg->accumulate_tail < block ? cfg->accumulate_tail : block - 1)
                          : 0;
+    const int tail_chunk =
+        cfg->accumulate_tail_chunk < tail ? cfg->accumulate_tail_chunk : tail;
     const int single = cfg->frame_spp <= 0 && chunk >= cfg->spp && tail == 0;
     double sum[3] = {0.0, 0.0, 0.0};
     v3 part = V(0.0f, 0.0f, 0.0f);
@@ -356,8 +360,7 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
         if (c0 < tail_start)
             c1 = c0 + chunk < tail_start ? c0 + chunk : tail_start;
         else
-            c1 = c0 + cfg->accumulate_tail_chunk < block_end ? c0 + cfg->accumulate_tail_chunk
-                                                             : block_end;
+            c1 = c0 + tail_chunk < block_end ? c0 + tail_chunk : block_end;
         for (int i = c0; i < c1; i++) {
             float jx = job->jitter[2 * i], jy = job->jitter[2 * i + 1];
             v3 rs = vadd(vscale(jx, du), vscale(jy, dv));

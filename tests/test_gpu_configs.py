@@ -14,6 +14,8 @@ ABI), per-channel RMS <= 1e-4 against the reference's sequential fp32 sum (north
 whole-frame properties (alpha 1, finite, radiance in [0, 1] for these scenes, segment counts
 between one and `depth` per sample). Reference loops: shader.comp:46-56, functions.glsl:73-91.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -131,6 +133,53 @@ def test_c4_sharded_eight_ways_equals_one_gpu(oracle):
                 torch.cuda.synchronize()
     check_subset(frame.cpu().numpy(), full, "c4 8-way shards vs 1 GPU")
     assert segs == st1["segments"]
+
+
+def read_pfm(path):
+    """PFM (linear rgb float32, little-endian, rows bottom to top) -> float32 [H, W, 3]."""
+    with open(path, "rb") as f:
+        data = f.read()
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"PF" and float(parts[2]) < 0  # colour, little-endian
+    w, h = (int(v) for v in parts[1].split())
+    img = np.frombuffer(parts[3], dtype="<f4", count=w * h * 3).reshape(h, w, 3)
+    return img[::-1].copy()
+
+
+@pytest.mark.parametrize("configured", [False, True])
+def test_cpp_host_api_reference_configuration_whole_frame(oracle, tmp_path, configured):
+    """The C++ host API of the reference (Renderer.hpp:14-20: BeginRenderingOperation /
+    DrawNextFrame / EndRenderingOperation, csrc/Renderer.cpp) driven by bin/vcrt_render, the
+    headless main() (VulkanComputeRayTracing.cpp:17-42), at the reference's own shipped
+    configuration: 1280x720, 1 spp, depth 50, its camera and its world[] (globals.glsl:9-24,
+    29-518; Common.hpp:23-24). Without options vcrt_render sets nothing, exactly as the
+    reference's main(); with them it goes through SetRenderDescription / SetRenderScene. At
+    1 spp the GPU runs one chunk per pixel -- the reference's own arithmetic (sum, then divide
+    by SAMPLES_PER_PIXEL) -- so the WHOLE frame is compared bit for bit with the oracle, over
+    two DrawNextFrame calls (each frame re-renders the same image, Linux.cpp:362-366)."""
+    import re
+    import subprocess
+    from vulkancomputeraytracing_amd import _native as N
+    w, h, spp, depth = 1280, 720, 1, 50
+    out = tmp_path / "frame.pfm"
+    cmd = [os.path.join(N.BIN_DIR, "vcrt_render"), "--frames", "2", "--out", str(out)]
+    if configured:
+        cmd += ["--width", str(w), "--height", str(h), "--spp", str(spp), "--depth", str(depth),
+                "--scene", "final"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    lines = res.stdout.strip().splitlines()
+    assert len(lines) == 2
+    segs = set()
+    for f, line in enumerate(lines):
+        m = re.match(r"frame (\d+): VK_SUCCESS .* (\d+) segments$", line)
+        assert m and int(m.group(1)) == f, line
+        segs.add(int(m.group(2)))
+    got = read_pfm(out)
+    assert got.shape == (h, w, 3)
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("final"))
+    check_subset(got, want[..., :3], f"vcrt_render {'configured' if configured else 'defaults'}")
+    assert segs == {want_segs}
 
 
 def test_c5_stress_pixel_grid(oracle):

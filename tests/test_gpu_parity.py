@@ -557,6 +557,35 @@ def test_rccl_comm_inside_libvcrt_world1(oracle):
     assert st["segments"] == segs
 
 
+def test_rccl_comm_missing_peer_fails_within_deadline(oracle, monkeypatch):
+    """The communicator is non-blocking with a deadline (csrc/comm_wait.hpp): rank 0 of a
+    2-rank world whose peer never joins gets VK_ERROR_INITIALIZATION_FAILED from vcrt_comm_init
+    once VCRT_COMM_TIMEOUT_MS has passed -- instead of blocking forever -- the communicator is
+    aborted, and the renderer goes on drawing its own shard (no gather), equal to the oracle's
+    pixels. (The reference bubbles every error up as a VkResult: VulkanComputeRayTracing.cpp:
+    20-35.)"""
+    import time
+    monkeypatch.setenv("VCRT_COMM_TIMEOUT_MS", "3000")
+    w, h, spp, depth, world = 64, 40, 2, 10, 2
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         rank=0, world_size=world)
+    cid = vc.renderer.comm_unique_id()
+    with vc.Renderer(desc, "final") as r:
+        t0 = time.monotonic()
+        with pytest.raises(vc.VcrtError) as err:
+            r.comm_init(cid)
+        dt = time.monotonic() - t0
+        assert err.value.code == N.VK_ERROR_INITIALIZATION_FAILED
+        assert 2.5 <= dt < 60.0
+        r.draw_next_frame()  # the shard still renders, without a gather
+        part, st = r.read_framebuffer(), r.stats()
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
+                            oracle.scene("final"))
+    m = vc.tile_pixel_map(w, h, world)
+    mine = m[..., 0] == 0
+    assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], "rank 0 after comm failure")
+
+
 def test_bench_single_gpu_validates_against_oracle():
     """bench.py at N = 1 with --validate: the rows it checks are the oracle's, bit for bit."""
     import json

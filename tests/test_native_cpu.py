@@ -87,6 +87,31 @@ def test_final_scene_generated_part_matches_golden():
     assert np.array_equal(flat.view(np.uint32), want.view(np.uint32))
 
 
+def _sphere_rows(s):
+    return np.concatenate([s["center"], s["radius"][:, None], s["colour"], s["texture"]], axis=1)
+
+
+def test_final_scene_equals_reference_world_table(oracle):
+    """The whole of the reference's `const sphere world[]` (globals.glsl:29-518: the 481
+    SceneGenerator lines, the big three at :513-515 and the ground at :517), parsed from the
+    reference file into tests/golden/world_globals_glsl.npy by make_world_fixture.py, equals the
+    product's final scene and the oracle's, value for value and in the same order (the order
+    decides ties: functions.glsl:27-29, 77)."""
+    want = np.load(os.path.join(GOLDEN, "world_globals_glsl.npy"))
+    meta = json.load(open(os.path.join(GOLDEN, "world_globals_glsl.json")))
+    assert want.shape == (485, 10) and want.dtype == np.float32
+    assert hashlib.sha256(want.tobytes()).hexdigest() == meta["table_sha256"]
+    assert meta["row_source_lines"]["ground"] == 517
+    for got in (vc.builtin_scene("final"), oracle.scene("final")):
+        assert np.array_equal(_sphere_rows(got).view(np.uint32), want.view(np.uint32))
+    # the built-in three-material scene is the table's tail (globals.glsl:513-517)
+    assert np.array_equal(_sphere_rows(vc.builtin_scene("three")).view(np.uint32),
+                          want[481:].view(np.uint32))
+    # the stress scene ends with the same four spheres
+    assert np.array_equal(_sphere_rows(vc.builtin_scene("stress4096")[-4:]).view(np.uint32),
+                          want[481:].view(np.uint32))
+
+
 def test_unknown_scene_is_an_error():
     assert N.lib().vcrt_scene_builtin(99, None, 0) == N.VK_ERROR_FEATURE_NOT_PRESENT
 
@@ -185,12 +210,13 @@ def test_work_chunk_rule(w, h, spp):
 
 
 @pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (1, 1)])
-@pytest.mark.parametrize("spp", [1, 16, 64, 256, 1024, 4096])
+@pytest.mark.parametrize("spp", [1, 16, 64, 256, 1024, 4096, 32768, 100000])
 def test_work_tail_rule(w, h, spp):
     """vcrt_work_tail (the tail of the chunk partition; host only): the same for every rank,
     restated here -- T = 6 * K * 327680 / (64 * the largest rank's tiles) to the nearest power of
-    two, items of max(4, K / 8) samples, none when 4 T > spp or K >= spp -- and explicit values
-    (capped below spp) or -1 (none) taken as given."""
+    two, items of max(4, K / 8) samples, none when 4 T > spp or K >= spp, the items grown until
+    head and tail take at most 512 chunks per pixel -- and explicit values (capped below spp) or
+    -1 (none) taken as given."""
     import math
     for world in (1, 2, 3, 8):
         parts = set()
@@ -207,8 +233,18 @@ def test_work_tail_rule(w, h, spp):
             want = 1 << round(math.log2(raw))
             if 4 * want > spp:
                 want = 0
+        want_kt = min(max(4, k // 8), want) if want else 0
+        if want:
+            room = 512 - -(-(spp - want) // k)
+            if -(-want // want_kt) > room:
+                if room > 0:
+                    want_kt = -(-want // room)
+                else:
+                    want, want_kt = 0, 0
         assert t == want
-        assert kt == (min(max(4, k // 8), t) if t else 0)
+        assert kt == want_kt
+        # what vcrt_begin accepts: at most 512 chunks per pixel, head and tail together
+        assert -(-(spp - t) // k) + (-(-t // kt) if t else 0) <= 512
         d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world,
                           accumulate_chunk=k, accumulate_tail=5, accumulate_tail_chunk=2)
         t5 = vc.renderer.work_tail(d)

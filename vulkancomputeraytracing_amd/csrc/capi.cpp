@@ -23,6 +23,7 @@
 
 #include "Shader.hpp"
 #include "cluster.hpp"
+#include "comm_wait.hpp"
 #include "hip_status.hpp"
 #include "scene.hpp"
 #include "vcrt.h"
@@ -103,7 +104,9 @@ struct RendererState {
     uint32_t pad_tiles = 0;     // tiles of the largest rank: the packed framebuffers' size
     // multi-GPU, one process per GPU (vcrt_comm_init): the ranks' packed framebuffers go to
     // rank 0 in one grouped RCCL send/recv inside vcrt_draw_next_frame; rank 0 assembles them
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;  // non-blocking (comm_wait.hpp): every wait has a deadline
+    bool comm_lost = false;     // the communicator failed or timed out and was aborted: every
+                                // later draw returns VK_ERROR_DEVICE_LOST (until vcrt_begin)
     float4* d_gather = nullptr;  // rank 0: [world][pad_tiles][64], its own tiles in slot 0
     float4* d_frame = nullptr;   // rank 0: the assembled frame [height][width]
     hipEvent_t ev_gather_start = nullptr, ev_gather = nullptr;
@@ -194,8 +197,20 @@ int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk)
         t = 1 << static_cast<int>(std::lround(std::log2(raw)));  // nearest power of two
         if (4 * static_cast<int64_t>(t) > spp) return 0;
     }
-    if (kt <= 0) kt = std::max(4, chunk / 8);
-    *tail_chunk = std::min(kt, t);
+    const bool kt_rule = kt <= 0;
+    if (kt_rule) kt = std::max(4, chunk / 8);
+    kt = std::min(kt, t);
+    // A pixel takes at most kAccumMaxChunks chunks, head and tail together (vcrt_begin rejects
+    // more). The head alone fits (default_chunk keeps spp / K <= 512). When the tail does not
+    // fit beside it, a rule-made tail item grows until it does; a rule-made tail that cannot fit
+    // is dropped; explicit values stay as given (vcrt_begin then reports them).
+    const int32_t head = (spp - t + chunk - 1) / chunk;
+    const int32_t room = vcrt::kAccumMaxChunks - head;
+    if ((t + kt - 1) / kt > room) {
+        if (room > 0 && kt_rule) kt = (t + room - 1) / room;
+        else if (d.accumulate_tail == 0) return 0;
+    }
+    *tail_chunk = kt;
     return t;
 }
 
@@ -387,38 +402,193 @@ VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Pa
     return VK_SUCCESS;
 }
 
+// State of the non-blocking communicator's last operations (comm_wait.hpp): done, still in
+// progress, or failed (an asynchronous error: a peer died, a network error).
+vcrt::PollState comm_state(ncclComm_t comm) {
+    ncclResult_t a = ncclSuccess;
+    if (ncclCommGetAsyncError(comm, &a) != ncclSuccess) return vcrt::PollState::kFailed;
+    return a == ncclSuccess      ? vcrt::PollState::kDone
+           : a == ncclInProgress ? vcrt::PollState::kPending
+                                 : vcrt::PollState::kFailed;
+}
+
+// Drops the communicator and the gather buffers. abort: ncclCommAbort, which also stops
+// operations still running on the device (a receive whose peer is gone), so that the render
+// stream drains; else a finalize (bounded) and destroy. Rank 0 renders into its own buffer again.
+void comm_release(bool abort) {
+    if (g.comm) {
+        if (!abort) {
+            const ncclResult_t f = ncclCommFinalize(g.comm);
+            abort = (f != ncclSuccess && f != ncclInProgress) ||
+                    vcrt::wait_with_deadline([] { return comm_state(g.comm); },
+                                             vcrt::comm_timeout_ms()) != vcrt::WaitResult::kDone;
+        }
+        (void)(abort ? ncclCommAbort(g.comm) : ncclCommDestroy(g.comm));
+        g.comm = nullptr;
+    }
+    if (g.stream) (void)hipStreamSynchronize(g.stream);
+    if (g.d_gather) (void)hipFree(g.d_gather);
+    if (g.d_frame) (void)hipFree(g.d_frame);
+    if (g.ev_gather) (void)hipEventDestroy(g.ev_gather);
+    if (g.ev_gather_start) (void)hipEventDestroy(g.ev_gather_start);
+    g.d_gather = nullptr;
+    g.d_frame = nullptr;
+    g.ev_gather = nullptr;
+    g.ev_gather_start = nullptr;
+    g.d_fb = g.d_fb_own;
+}
+
+// A communicator failure inside a draw: abort it and report the device lost (the reference's
+// errors bubble up as VkResult, VulkanComputeRayTracing.cpp:20-35).
+VkResult comm_fail() {
+    comm_release(true);
+    g.comm_lost = true;
+    return VK_ERROR_DEVICE_LOST;
+}
+
 // The frame gather, stream-ordered after the trace and resolve: every rank's
 // packed tiles (pad_tiles x 64 float4, 4.1 MB per rank at 1080p / 8 GPUs) go to rank 0 in one
 // grouped send/recv, so rank 0 receives from all peers at once over their own xGMI links
 // (a ring all-gather would move the whole frame through every rank); rank 0 then
-// re-interleaves the frame (vcrt_assemble). Every rank takes part, whatever its share.
+// re-interleaves the frame (vcrt_assemble). Every rank takes part, whatever its share. The
+// communicator is non-blocking: the group is enqueued when its state leaves ncclInProgress
+// (bounded wait), and the caller waits for ev_gather with a deadline (wait_gather).
 VkResult gather_frame() {
     VCRT_TRY(hipEventRecord(g.ev_gather_start, g.stream));
     const size_t n = static_cast<size_t>(g.pad_tiles) * 64 * 4;  // floats per rank
-    VkResult r = nccl_vk(ncclGroupStart());
-    if (r != VK_SUCCESS) return r;
-    if (g.desc.rank == 0) {
-        for (int32_t peer = 1; peer < g.desc.world_size && r == VK_SUCCESS; peer++)
-            r = nccl_vk(ncclRecv(reinterpret_cast<float*>(g.d_gather) + n * peer, n,
-                                 ncclFloat32, peer, g.comm, g.stream));
-    } else {
-        r = nccl_vk(ncclSend(g.d_fb, n, ncclFloat32, 0, g.comm, g.stream));
+    auto ok = [](ncclResult_t e) { return e == ncclSuccess || e == ncclInProgress; };
+    bool good = ok(ncclGroupStart());
+    if (good) {
+        if (g.desc.rank == 0) {
+            for (int32_t peer = 1; peer < g.desc.world_size && good; peer++)
+                good = ok(ncclRecv(reinterpret_cast<float*>(g.d_gather) + n * peer, n,
+                                   ncclFloat32, peer, g.comm, g.stream));
+        } else {
+            good = ok(ncclSend(g.d_fb, n, ncclFloat32, 0, g.comm, g.stream));
+        }
+        good = ok(ncclGroupEnd()) && good;
     }
-    const VkResult r_end = nccl_vk(ncclGroupEnd());
-    if (r != VK_SUCCESS) return r;
-    if (r_end != VK_SUCCESS) return r_end;
+    if (!good || vcrt::wait_with_deadline([] { return comm_state(g.comm); },
+                                          vcrt::comm_timeout_ms()) != vcrt::WaitResult::kDone)
+        return comm_fail();
     if (g.desc.rank == 0) {
         vcrt::AssembleParams ap{g.d_gather,    g.d_frame,         g.desc.width,
                                 g.desc.height, g.desc.world_size, g.tiles_x,
                                 g.pad_tiles};
         const uint64_t total = static_cast<uint64_t>(g.desc.width) * g.desc.height;
-        r = launch(g.k_assemble,
-                   static_cast<uint32_t>(std::min<uint64_t>((total + 255) / 256, 8192)), 256, 0,
-                   ap);
+        const VkResult r = launch(
+            g.k_assemble, static_cast<uint32_t>(std::min<uint64_t>((total + 255) / 256, 8192)),
+            256, 0, ap);
         if (r != VK_SUCCESS) return r;
     }
     VCRT_TRY(hipEventRecord(g.ev_gather, g.stream));
     return VK_SUCCESS;
+}
+
+// Waits for the gather recorded by gather_frame, polling the communicator's asynchronous error
+// beside the event: a peer that never sends makes this return VK_ERROR_DEVICE_LOST (after
+// aborting the communicator) at the deadline instead of blocking forever.
+VkResult wait_gather() {
+    hipError_t ev = hipSuccess;
+    const vcrt::WaitResult w = vcrt::wait_with_deadline(
+        [&ev] {
+            ev = hipEventQuery(g.ev_gather);
+            if (ev == hipSuccess) return vcrt::PollState::kDone;
+            if (ev != hipErrorNotReady) return vcrt::PollState::kFailed;
+            return comm_state(g.comm) == vcrt::PollState::kFailed ? vcrt::PollState::kFailed
+                                                                  : vcrt::PollState::kPending;
+        },
+        vcrt::comm_timeout_ms());
+    if (w == vcrt::WaitResult::kDone) return VK_SUCCESS;
+    if (w == vcrt::WaitResult::kFailed && ev != hipSuccess && ev != hipErrorNotReady) {
+        const VkResult r = to_vk(ev);  // the device itself failed
+        comm_fail();
+        return r;
+    }
+    return comm_fail();
+}
+
+// The tracer kernel a draw launches for the current scene and desc: variant (AUTO resolved),
+// entry point, block size and dynamic LDS.
+struct KernelChoice {
+    hipFunction_t f, stats;
+    const char* name;
+    uint32_t block, lds;
+    int variant;
+};
+
+KernelChoice select_kernel() {
+    // scan table: (groups + 1 padding group) x 64 B
+    const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
+    // per-lane culled scan: tables in LDS. Up to 32 KB with 256-thread workgroups (5 per
+    // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
+    // copy for 16 waves); beyond that from global memory.
+    const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
+    // flat: near/far boxes (80 B per pair), 64-B group records, uint16 member indices
+    const uint32_t tab_lds_flat =
+        static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 4) + 8 * g.ncgroups);
+    const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
+    const bool lane_wide = lane_lds && tab_lds > 32768u;
+    int variant = g.desc.kernel_variant;
+    // Measured on MI355X (1080p, box hierarchy): of the linear scans the scalar-cache
+    // variant (sphere data in SGPRs, no LDS traffic) beats LDS staging by 15% (485
+    // spheres) and 18% (4100); the culled scans beat both (same bits). AUTO: the flattened
+    // scan (485 spheres: 3.3x SMEM, +14% over CULL_LANE, +28% over CULL; 4100 spheres with
+    // its tables in global memory), and SMEM when the scene has no tables (< 16 spheres or
+    // unbounded).
+    if (variant == VCRT_KERNEL_AUTO)
+        variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_FLAT;
+    if (variant == VCRT_KERNEL_LDS && geom_lds > g.max_lds) variant = VCRT_KERNEL_SMEM;
+    if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE ||
+         variant == VCRT_KERNEL_CULL_FLAT) &&
+        g.ncgroups == 0)
+        variant = VCRT_KERNEL_SMEM;
+    // The flat scan keeps 4.25 KB of stacks per wave in LDS beside its tables when they fit
+    // in 32 KB (16-bit entries), in 256-thread workgroups (five per CU, each with its copy of
+    // the tables). Otherwise the tables stay in global memory and the stacks take 32-bit
+    // entries (6.75 KB per wave).
+    const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
+                          g.ncgroups <= vcrt::kFlatMaxGroups;
+    hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
+    const char* fname = "vcrt_trace_smem";
+    uint32_t block = 256;
+    uint32_t lds = 0;
+    if (variant == VCRT_KERNEL_LDS) {
+        f = g.k_trace_lds;
+        fs = g.k_trace_lds_stats;
+        fname = "vcrt_trace_lds";
+        lds = geom_lds;
+    } else if (variant == VCRT_KERNEL_CULL) {
+        f = g.k_trace_cull;
+        fs = g.k_trace_cull_stats;
+        fname = "vcrt_trace_cull";
+    } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_lds) {
+        f = g.k_trace_cull_flat;
+        fs = g.k_trace_cull_flat_stats;
+        fname = "vcrt_trace_cull_flat";
+        lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
+    } else if (variant == VCRT_KERNEL_CULL_FLAT) {
+        f = g.k_trace_cull_flat_global;
+        fs = g.k_trace_cull_flat_global_stats;
+        fname = "vcrt_trace_cull_flat_global";
+        lds = 4 * vcrt::kWaveScratchBytesWide;
+    } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
+        f = g.k_trace_cull_lane_lds_wide;
+        fs = g.k_trace_cull_lane_lds_wide_stats;
+        fname = "vcrt_trace_cull_lane_lds_wide";
+        block = 1024;
+        lds = tab_lds;
+    } else if (variant == VCRT_KERNEL_CULL_LANE && lane_lds) {
+        f = g.k_trace_cull_lane_lds;
+        fs = g.k_trace_cull_lane_lds_stats;
+        fname = "vcrt_trace_cull_lane_lds";
+        lds = tab_lds;
+    } else if (variant == VCRT_KERNEL_CULL_LANE) {
+        f = g.k_trace_cull_lane;
+        fs = g.k_trace_cull_lane_stats;
+        fname = "vcrt_trace_cull_lane";
+    }
+    return KernelChoice{f, fs, fname, block, lds, variant};
 }
 
 }  // namespace
@@ -720,11 +890,13 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         if (!(std::fabs(sp.radius) >= 0x1p-40f && std::fabs(sp.radius) <= 0x1p30f))
             g.radii_safe = false;
     }
+    g.stage.pName = select_kernel().name;  // the entry point draws of this scene dispatch
     return VCRT_SUCCESS;
 }
 
 vcrt_result vcrt_draw_next_frame(void) {
     if (!g.begun || !g.stage.module) return VCRT_ERROR_INITIALIZATION_FAILED;
+    if (g.comm_lost) return VCRT_ERROR_DEVICE_LOST;  // a peer was lost in an earlier frame
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t pixels = g.total_pixels;
     g.stats.segments = 0;
@@ -801,82 +973,13 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.spp_total = static_cast<float>(spp_total);
         const std::array<float, 12> cam = camera_array();
         for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
-        // scan table: (groups + 1 padding group) x 64 B
-        const uint32_t geom_lds = static_cast<uint32_t>(64 * ((g.nspheres + 3) / 4 + 1));
-        // per-lane culled scan: tables in LDS. Up to 32 KB with 256-thread workgroups (5 per
-        // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
-        // copy for 16 waves); beyond that from global memory. Every kernel also keeps its waves'
-        // sample sums in LDS (kWaveAccumBytes per wave, ahead of the tables).
-        const uint32_t acc4 = 0, acc16 = 0;
-        const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
-        // flat: near/far boxes (80 B per pair), 64-B group records, uint16 member indices
-        const uint32_t tab_lds_flat =
-            static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 4) + 8 * g.ncgroups);
-        const bool lane_lds = tab_lds + acc16 <= g.max_lds && g.cull_lane_tables != 2;
-        const bool lane_wide = lane_lds && tab_lds + acc4 > 32768u;
-        int variant = g.desc.kernel_variant;
-        // Measured on MI355X (1080p, box hierarchy): of the linear scans the scalar-cache
-        // variant (sphere data in SGPRs, no LDS traffic) beats LDS staging by 15% (485
-        // spheres) and 18% (4100); the culled scans beat both (same bits). AUTO: the flattened
-        // scan (485 spheres: 3.3x SMEM, +14% over CULL_LANE, +28% over CULL; 4100 spheres with
-        // its tables in global memory), and SMEM when the scene has no tables (< 16 spheres or
-        // unbounded).
-        if (variant == VCRT_KERNEL_AUTO)
-            variant = g.ncgroups == 0 ? VCRT_KERNEL_SMEM : VCRT_KERNEL_CULL_FLAT;
-        if (variant == VCRT_KERNEL_LDS && geom_lds + acc4 > g.max_lds) variant = VCRT_KERNEL_SMEM;
-        if ((variant == VCRT_KERNEL_CULL || variant == VCRT_KERNEL_CULL_LANE ||
-             variant == VCRT_KERNEL_CULL_FLAT) &&
-            g.ncgroups == 0)
-            variant = VCRT_KERNEL_SMEM;
-        // The flat scan keeps 4 KB of stacks per wave in LDS beside its tables when they fit in
-        // 32 KB (16-bit entries), in 640-thread workgroups: two per CU (20 waves) share two
-        // copies of the tables, where five 256-thread workgroups would need five. Otherwise the
-        // tables stay in global memory and the stacks take 32-bit entries (6.25 KB per wave).
-        const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
-                              g.ncgroups <= vcrt::kFlatMaxGroups;
-        hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
-        const char* fname = "vcrt_trace_smem";
-        uint32_t block = 256;
-        uint32_t lds = acc4;
-        if (variant == VCRT_KERNEL_LDS) {
-            f = g.k_trace_lds;
-            fs = g.k_trace_lds_stats;
-            fname = "vcrt_trace_lds";
-            lds = acc4 + geom_lds;
-        } else if (variant == VCRT_KERNEL_CULL) {
-            f = g.k_trace_cull;
-            fs = g.k_trace_cull_stats;
-            fname = "vcrt_trace_cull";
-        } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_lds) {
-            f = g.k_trace_cull_flat;
-            fs = g.k_trace_cull_flat_stats;
-            fname = "vcrt_trace_cull_flat";
-            lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
-        } else if (variant == VCRT_KERNEL_CULL_FLAT) {
-            f = g.k_trace_cull_flat_global;
-            fs = g.k_trace_cull_flat_global_stats;
-            fname = "vcrt_trace_cull_flat_global";
-            lds = 4 * vcrt::kWaveScratchBytesWide;
-        } else if (variant == VCRT_KERNEL_CULL_LANE && lane_wide) {
-            f = g.k_trace_cull_lane_lds_wide;
-            fs = g.k_trace_cull_lane_lds_wide_stats;
-            fname = "vcrt_trace_cull_lane_lds_wide";
-            block = 1024;
-            lds = acc16 + tab_lds;
-        } else if (variant == VCRT_KERNEL_CULL_LANE && lane_lds) {
-            f = g.k_trace_cull_lane_lds;
-            fs = g.k_trace_cull_lane_lds_stats;
-            fname = "vcrt_trace_cull_lane_lds";
-            lds = acc4 + tab_lds;
-        } else if (variant == VCRT_KERNEL_CULL_LANE) {
-            f = g.k_trace_cull_lane;
-            fs = g.k_trace_cull_lane_stats;
-            fname = "vcrt_trace_cull_lane";
-        }
-        if (g.debug_stats == 1) f = fs;
+        const KernelChoice kc = select_kernel();
+        hipFunction_t f = g.debug_stats == 1 ? kc.stats : kc.f;
+        const uint32_t block = kc.block, lds = kc.lds;
+        const int variant = kc.variant;
         // the stage names the entry point this draw dispatches (Shader.cpp:89 names "main")
-        g.stage.pName = fname;
-        std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s%s", fname,
+        g.stage.pName = kc.name;
+        std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s%s", kc.name,
                       g.debug_stats == 1 ? "_stats" : "");
         int per_cu = g.desc.blocks_per_cu;
         if (per_cu <= 0) {
@@ -934,9 +1037,9 @@ vcrt_result vcrt_draw_next_frame(void) {
                                  f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
     }
     if (g.comm && g.desc.world_size > 1) {
-        const VkResult r = gather_frame();
+        VkResult r = gather_frame();
+        if (r == VK_SUCCESS) r = wait_gather();
         if (r != VK_SUCCESS) return r;
-        VCRT_TRY(hipStreamSynchronize(g.stream));
         float ms = 0.f;
         VCRT_TRY(hipEventElapsedTime(&ms, g.ev_gather_start, g.ev_gather));
         g.stats.gather_ms = ms;
@@ -970,11 +1073,7 @@ vcrt_result vcrt_end(void) {
     if (g.d_accum) (void)hipFree(g.d_accum);
     if (g.d_srgb_thresholds) (void)hipFree(g.d_srgb_thresholds);
     if (g.d_srgb) (void)hipFree(g.d_srgb);
-    if (g.comm) (void)ncclCommDestroy(g.comm);
-    if (g.d_gather) (void)hipFree(g.d_gather);
-    if (g.d_frame) (void)hipFree(g.d_frame);
-    if (g.ev_gather) (void)hipEventDestroy(g.ev_gather);
-    if (g.ev_gather_start) (void)hipEventDestroy(g.ev_gather_start);
+    comm_release(false);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = RendererState{};
     return VCRT_SUCCESS;
@@ -997,20 +1096,38 @@ vcrt_result vcrt_comm_init(const vcrt_comm_id* id) {
     VCRT_TRY(hipStreamSynchronize(g.stream));
     ncclUniqueId u;
     std::memcpy(u.internal, id->internal, sizeof(u.internal));
-    VkResult r = nccl_vk(ncclCommInitRank(&g.comm, g.desc.world_size, u, g.desc.rank));
-    if (r != VK_SUCCESS) {
+    // non-blocking: set-up and every later operation are waited for with a deadline
+    // (comm_wait.hpp), so a rank that never joins fails this call instead of hanging it
+    ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+    config.blocking = 0;
+    const ncclResult_t e = ncclCommInitRankConfig(&g.comm, g.desc.world_size, u, g.desc.rank,
+                                                  &config);
+    if (e != ncclSuccess && e != ncclInProgress) {
+        if (g.comm) comm_release(true);
         g.comm = nullptr;
-        return r;
+        return nccl_vk(e);
     }
-    VCRT_TRY(hipEventCreate(&g.ev_gather_start));
-    VCRT_TRY(hipEventCreate(&g.ev_gather));
+    if (vcrt::wait_with_deadline([] { return comm_state(g.comm); }, vcrt::comm_timeout_ms()) !=
+        vcrt::WaitResult::kDone) {
+        comm_release(true);
+        return VCRT_ERROR_INITIALIZATION_FAILED;
+    }
+    // from here on every failure drops the communicator and the buffers (comm_release)
+    auto fail = [](hipError_t err) {
+        comm_release(true);
+        return to_vk(err);
+    };
+    hipError_t err;
+    if ((err = hipEventCreate(&g.ev_gather_start)) != hipSuccess) return fail(err);
+    if ((err = hipEventCreate(&g.ev_gather)) != hipSuccess) return fail(err);
     if (g.desc.world_size > 1 && g.desc.rank == 0) {
         const size_t slab = static_cast<size_t>(g.pad_tiles) * 64 * sizeof(float4);
-        VCRT_TRY(hipMalloc(&g.d_gather, slab * static_cast<size_t>(g.desc.world_size)));
-        VCRT_TRY(hipMemset(g.d_gather, 0, slab * static_cast<size_t>(g.desc.world_size)));
+        const size_t all = slab * static_cast<size_t>(g.desc.world_size);
+        if ((err = hipMalloc(&g.d_gather, all)) != hipSuccess) return fail(err);
+        if ((err = hipMemset(g.d_gather, 0, all)) != hipSuccess) return fail(err);
         const size_t frame = static_cast<size_t>(g.desc.width) * g.desc.height * sizeof(float4);
-        VCRT_TRY(hipMalloc(&g.d_frame, frame));
-        VCRT_TRY(hipMemset(g.d_frame, 0, frame));
+        if ((err = hipMalloc(&g.d_frame, frame)) != hipSuccess) return fail(err);
+        if ((err = hipMemset(g.d_frame, 0, frame)) != hipSuccess) return fail(err);
         g.d_fb = g.d_gather;  // rank 0 renders straight into its slot of the gather buffer
     } else {
         g.d_fb = g.d_fb_own;
@@ -1147,7 +1264,9 @@ vcrt_result vcrt_shader_load(const char* filename) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (!filename) return VCRT_ERROR_INCOMPATIBLE_SHADER_BINARY;
     (void)hipStreamSynchronize(g.stream);
-    return load_code_object(filename);
+    const VkResult r = load_code_object(filename);
+    if (r == VK_SUCCESS && g.d_geom) g.stage.pName = select_kernel().name;
+    return r;
 }
 
 int32_t vcrt_scene_builtin(int32_t scene_id, vcrt_sphere* out, int32_t cap) {

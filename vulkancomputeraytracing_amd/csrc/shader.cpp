@@ -43,9 +43,10 @@ VkResult CreateShaderStageFromFile(IN const char* filename, IN VkShaderStageFlag
     info->sType = 18;  // VK_STRUCTURE_TYPE_PIPELINE_SHADER_STAGE_CREATE_INFO
     info->stage = stage;
     info->module = module;
-    // the entry point vcrt_draw_next_frame dispatches for the reference's own scene (AUTO on
-    // the final scene); each draw then sets the stage's pName to the kernel it launched
-    info->pName = "vcrt_trace_cull_flat";
+    // The code object holds every tracer variant; which one is the entry point depends on the
+    // scene and the desc (capi.cpp select_kernel), so the renderer names it: after the scene is
+    // set (vcrt_set_scene, vcrt_shader_load) and at every draw. Unnamed until then.
+    info->pName = nullptr;
     return VK_SUCCESS;
 }
 

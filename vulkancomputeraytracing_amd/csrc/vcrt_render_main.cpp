@@ -27,10 +27,12 @@ int main(int argc, char** argv) {
     vcrt_default_desc(&desc);
     int scene = VCRT_SCENE_FINAL, frames = 1;
     std::string out;
+    bool configured = false;  // any option that changes the description or the scene
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
         if (i + 1 >= argc) return usage();
         const char* v = argv[++i];
+        configured = configured || (a != "--out" && a != "--frames");
         if (a == "--width") desc.width = std::atoi(v);
         else if (a == "--height") desc.height = std::atoi(v);
         else if (a == "--spp") desc.samples_per_pixel = std::atoi(v);
@@ -46,12 +48,17 @@ int main(int argc, char** argv) {
             if (scene < 0) return usage();
         } else return usage();
     }
-    std::vector<vcrt_sphere> world(8192);
-    const int n = vcrt_scene_builtin(scene, world.data(), static_cast<int32_t>(world.size()));
-    if (n < 0) return 1;
-    world.resize(n);
-    SetRenderDescription(&desc);
-    SetRenderScene(world.data(), n);
+    // Without options this is the reference's main() exactly: Begin/Draw/End with nothing set,
+    // so BeginRenderingOperation takes the reference's compile-time configuration (1280x720,
+    // 1 spp, depth 50, its camera: globals.glsl:9-24) and its world[] (the final scene).
+    if (configured) {
+        std::vector<vcrt_sphere> world(8192);
+        const int n = vcrt_scene_builtin(scene, world.data(), static_cast<int32_t>(world.size()));
+        if (n < 0) return 1;
+        world.resize(n);
+        SetRenderDescription(&desc);
+        SetRenderScene(world.data(), n);
+    }
     VkResult r = BeginRenderingOperation();
     if (r != VK_SUCCESS) {
         std::fprintf(stderr, "BeginRenderingOperation: %s\n", vcrt_result_string(r));

@@ -4,10 +4,14 @@ One process per GPU. The frame is cut into 8x8 tiles (tx, ty); rank r renders th
 (tx + ty) % world == r, so every work item stays a coherent 8x8 tile and every rank gets the
 same number of tiles (to one per row) spread over every row and column of the frame (sky and
 ground, left and right alike: SURVEY.md 8(e)).
-The packed rank framebuffers [tiles_per_rank][64] are gathered to rank 0 over RCCL
-(``torch.distributed`` backend "nccl") and rank 0 re-interleaves them with the vcrt_assemble
-HIP kernel. The reference is single-GPU (Environment.cpp:157-165; "TODO: Cross-GPU sharing",
-Frontend.cpp:107); the gather is the one exchange step of the path.
+The product's gather is inside libvcrt.so: after vcrt_comm_init, vcrt_draw_next_frame sends the
+packed rank framebuffers [tiles_per_rank][64] to rank 0 over RCCL (one grouped send/recv, on a
+non-blocking communicator with a deadline) and rank 0 re-interleaves them with the vcrt_assemble
+HIP kernel (capi.cpp gather_frame; bench.py drives it). This module keeps the tile helpers and a
+torch.distributed rehearsal of the same exchange (gather_tiles / assemble_frame), used with the
+"gloo" backend to run the N-rank flow on a box with fewer GPUs than ranks (RCCL needs one GPU per
+rank) and by the CPU tests. The reference is single-GPU (Environment.cpp:157-165; "TODO:
+Cross-GPU sharing", Frontend.cpp:107); the gather is the one exchange step of the path.
 """
 from __future__ import annotations
 
