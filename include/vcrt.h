@@ -258,6 +258,17 @@ int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom,
 int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt_render_desc* desc,
                            uint32_t* info, int32_t cap_tiles, uint16_t* ids, int32_t cap_ids);
 
+/* The camera fast trace's per-sphere lists (host only, no GPU; csrc/primary.cpp): for each 4x4
+ * quarter as above, info = first pair << 4 | spheres (<= 14), or 15 when it has no list, and the
+ * pair records, 12 floats each: (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1) (index0, index1 as
+ * int bits, 0, 0), camera-relative as the kernel's exact test computes them (oc = camera centre -
+ * centre, cc = |oc|^2 - r^2 in fp32; an odd list pads with oc = 0, cc = 3e38, index -1). Returns
+ * the number of pair records (-1: no culling tables, or an invalid desc), and writes info / rec
+ * when cap_tiles (entries) / cap_floats are large enough (pointers may be NULL). */
+int32_t vcrt_primary_sphere_lists(const vcrt_sphere* spheres, int32_t count,
+                                  const vcrt_render_desc* desc, uint32_t* info, int32_t cap_tiles,
+                                  float* rec, int32_t cap_floats);
+
 /* Device self-test of the kernel's fast sin path (tracer.hip vcrt_check_sin): for the fp32
  * inputs whose bit patterns are first .. first + count - 1, counts those where the device's
  * sin_fast differs from the canonical sin (must be 0) and those where it fell back to the

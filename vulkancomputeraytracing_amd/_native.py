@@ -152,6 +152,10 @@ SIGNATURES = {
     "vcrt_primary_lists": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32,
                                             ctypes.POINTER(vcrt_render_desc), ctypes.c_void_p,
                                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]),
+    "vcrt_primary_sphere_lists": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_int32,
+                                                   ctypes.POINTER(vcrt_render_desc),
+                                                   ctypes.c_void_p, ctypes.c_int32,
+                                                   ctypes.c_void_p, ctypes.c_int32]),
     "vcrt_canonical_sin": (ctypes.c_float, [ctypes.c_float]),
     "vcrt_canonical_rand": (ctypes.c_float, [ctypes.c_float, ctypes.c_float]),
     "vcrt_result_string": (ctypes.c_char_p, [ctypes.c_int32]),

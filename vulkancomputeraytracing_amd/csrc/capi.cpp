@@ -80,7 +80,7 @@ struct RendererState {
     float4* d_ctop = nullptr;
     uint32_t* d_prim_info = nullptr;  // camera-ray tile lists (primary.cpp), flat scan only
     uint16_t* d_prim_ids = nullptr;
-    float4* d_cam_oc = nullptr;  // camera-relative group records (build_camera_records)
+    float4* d_cam_rec = nullptr;  // camera-relative records: big groups, sphere lists
     bool primary_lists = true;        // VCRT_PRIMARY_LISTS=0 turns them off
     // work decomposition
     int32_t chunk = 1, nchunks = 1;
@@ -276,8 +276,8 @@ void free_scene() {
     if (g.d_ctop) (void)hipFree(g.d_ctop);
     if (g.d_prim_info) (void)hipFree(g.d_prim_info);
     if (g.d_prim_ids) (void)hipFree(g.d_prim_ids);
-    if (g.d_cam_oc) (void)hipFree(g.d_cam_oc);
-    g.d_cam_oc = nullptr;
+    if (g.d_cam_rec) (void)hipFree(g.d_cam_rec);
+    g.d_cam_rec = nullptr;
     g.d_prim_info = nullptr;
     g.d_prim_ids = nullptr;
     g.d_cgroup = nullptr;
@@ -844,22 +844,34 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         g.ncbig = ct.nbig;
         std::memcpy(g.cmargin, ct.margin, sizeof(ct.margin));
         if (g.primary_lists && g.local_tiles > 0) {
-            // camera rays of a tile start from its group list (primary.cpp)
+            // camera rays of a tile start from its quarter's lists (primary.cpp): the groups
+            // for the main scan, the spheres for the camera fast trace; info interleaved
             vcrt::PrimaryLists pl;
             vcrt::build_primary_lists(ct, camera_array().data(), g.desc.width, g.desc.height,
                                       g.desc.rank, g.desc.world_size, pl);
-            VCRT_TRY(hipMalloc(&g.d_prim_info, sizeof(uint32_t) * pl.info.size()));
-            VCRT_TRY(hipMemcpy(g.d_prim_info, pl.info.data(), sizeof(uint32_t) * pl.info.size(),
+            vcrt::PrimarySphereLists sl;
+            vcrt::build_primary_sphere_lists(ct, spheres, camera_array().data(), g.desc.width,
+                                             g.desc.height, g.desc.rank, g.desc.world_size, sl);
+            std::vector<uint32_t> info(2 * pl.info.size());
+            for (size_t e = 0; e < pl.info.size(); e++) {
+                info[2 * e] = pl.info[e];
+                info[2 * e + 1] = sl.info[e];
+            }
+            VCRT_TRY(hipMalloc(&g.d_prim_info, sizeof(uint32_t) * info.size()));
+            VCRT_TRY(hipMemcpy(g.d_prim_info, info.data(), sizeof(uint32_t) * info.size(),
                                hipMemcpyHostToDevice));
             VCRT_TRY(hipMalloc(&g.d_prim_ids, sizeof(uint16_t) * (pl.ids.size() + 1)));
             if (!pl.ids.empty())
                 VCRT_TRY(hipMemcpy(g.d_prim_ids, pl.ids.data(), sizeof(uint16_t) * pl.ids.size(),
                                    hipMemcpyHostToDevice));
-            // the camera fast trace's camera-relative group records
+            // the camera fast trace's records: the big groups', then the sphere lists' pairs
             std::vector<float> crec;
             vcrt::build_camera_records(ct, camera_array().data(), crec);
-            VCRT_TRY(hipMalloc(&g.d_cam_oc, sizeof(float) * crec.size()));
-            VCRT_TRY(hipMemcpy(g.d_cam_oc, crec.data(), sizeof(float) * crec.size(),
+            crec.resize(static_cast<size_t>(ct.nbig) * 16);
+            crec.insert(crec.end(), sl.rec.begin(), sl.rec.end());
+            crec.resize(crec.size() + 12, 0.0f);  // never empty
+            VCRT_TRY(hipMalloc(&g.d_cam_rec, sizeof(float) * crec.size()));
+            VCRT_TRY(hipMemcpy(g.d_cam_rec, crec.data(), sizeof(float) * crec.size(),
                                hipMemcpyHostToDevice));
         }
     }
@@ -947,7 +959,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.ctop = g.d_ctop;
         p.prim_info = g.d_prim_info;
         p.prim_ids = g.d_prim_ids;
-        p.cam_oc = g.d_cam_oc;
+        p.cam_rec = g.d_cam_rec;
         p.ncgroups = g.ncgroups;
         p.nbig = g.ncbig;
         for (int k = 0; k < 4; k++) p.box_margin[k] = g.cmargin[k];
@@ -1307,11 +1319,12 @@ int32_t vcrt_cull_tables(const vcrt_sphere* spheres, int32_t count, float* geom,
     return ct.ngroups;
 }
 
-int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt_render_desc* desc,
-                           uint32_t* info, int32_t cap_tiles, uint16_t* ids, int32_t cap_ids) {
-    if (!desc || !desc_valid(*desc) || count < 0 || (count > 0 && !spheres)) return -1;
-    vcrt::CullTables ct;
-    if (!vcrt::build_cull_tables(spheres, count, ct)) return -1;
+namespace {
+// Culling tables and the kernels' camera array for a desc (host only).
+bool host_camera_tables(const vcrt_sphere* spheres, int32_t count, const vcrt_render_desc* desc,
+                        vcrt::CullTables& ct, float cam[12]) {
+    if (!desc || !desc_valid(*desc) || count < 0 || (count > 0 && !spheres)) return false;
+    if (!vcrt::build_cull_tables(spheres, count, ct)) return false;
     const vcrt_camera& c = desc->camera;
     const vcrt::Camera cm = vcrt::make_camera(desc->width, desc->height,
                                               vcrt::mk(c.lookfrom[0], c.lookfrom[1], c.lookfrom[2]),
@@ -1319,12 +1332,20 @@ int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt
                                               vcrt::mk(c.vup[0], c.vup[1], c.vup[2]), c.vfov,
                                               [](double x) { return std::tan(x); });
     const vcrt::f3 v[4] = {cm.pixel00, cm.delta_u, cm.delta_v, cm.center};
-    float cam[12];
     for (int i = 0; i < 4; i++) {
         cam[3 * i + 0] = v[i].x;
         cam[3 * i + 1] = v[i].y;
         cam[3 * i + 2] = v[i].z;
     }
+    return true;
+}
+}  // namespace
+
+int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt_render_desc* desc,
+                           uint32_t* info, int32_t cap_tiles, uint16_t* ids, int32_t cap_ids) {
+    vcrt::CullTables ct;
+    float cam[12];
+    if (!host_camera_tables(spheres, count, desc, ct, cam)) return -1;
     vcrt::PrimaryLists pl;
     vcrt::build_primary_lists(ct, cam, desc->width, desc->height, desc->rank, desc->world_size,
                               pl);
@@ -1333,6 +1354,22 @@ int32_t vcrt_primary_lists(const vcrt_sphere* spheres, int32_t count, const vcrt
     if (ids && cap_ids >= static_cast<int32_t>(pl.ids.size()))
         std::memcpy(ids, pl.ids.data(), sizeof(uint16_t) * pl.ids.size());
     return static_cast<int32_t>(pl.ids.size());
+}
+
+int32_t vcrt_primary_sphere_lists(const vcrt_sphere* spheres, int32_t count,
+                                  const vcrt_render_desc* desc, uint32_t* info, int32_t cap_tiles,
+                                  float* rec, int32_t cap_floats) {
+    vcrt::CullTables ct;
+    float cam[12];
+    if (!host_camera_tables(spheres, count, desc, ct, cam)) return -1;
+    vcrt::PrimarySphereLists sl;
+    vcrt::build_primary_sphere_lists(ct, spheres, cam, desc->width, desc->height, desc->rank,
+                                     desc->world_size, sl);
+    if (info && cap_tiles >= static_cast<int32_t>(sl.info.size()))
+        std::memcpy(info, sl.info.data(), sizeof(uint32_t) * sl.info.size());
+    if (rec && cap_floats >= static_cast<int32_t>(sl.rec.size()))
+        std::memcpy(rec, sl.rec.data(), sizeof(float) * sl.rec.size());
+    return static_cast<int32_t>(sl.rec.size() / 12);
 }
 
 float vcrt_canonical_sin(float x) { return vcrt::sin_canonical(x); }

@@ -49,6 +49,26 @@ struct PrimaryLists {
 void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
                          int32_t height, int32_t rank, int32_t world, PrimaryLists& out);
 
+// Per-sphere camera lists (round 3) for the camera fast trace: for every 4x4-pixel quarter of
+// every local tile, the hierarchy's spheres a camera ray through it may need (the members of its
+// group list whose sphere, grown by its own margin M_s = 8.1u (|oc|^2 + r^2) / r and 1e-3, no
+// side plane of the quarter's pyramid separates: primary.cpp), as camera-relative pair records:
+// per pair of spheres (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1) (index0,index1 as int bits,0,0),
+// evaluated as pair_disc_cc would (an odd count pads its last pair with oc = 0, cc = 3e38, index
+// -1: never a candidate). info[4 lt + 2 qy + qx] = first pair << 4 | spheres (<= 14), or
+// kPrimaryNone. On average ~1.1 spheres per quarter at the final scene's 1080p camera, against
+// ~10.6 members of the listed groups.
+constexpr uint32_t kPrimarySphereMax = 14;
+
+struct PrimarySphereLists {
+    std::vector<uint32_t> info;  // [4 x local tiles]
+    std::vector<float> rec;      // [pairs][12]
+};
+
+void build_primary_sphere_lists(const CullTables& ct, const vcrt_sphere* spheres,
+                                const float cam[12], int32_t width, int32_t height, int32_t rank,
+                                int32_t world, PrimarySphereLists& out);
+
 // Camera-relative group records for the camera fast trace: for every group of ct.geom (big
 // groups first), the members' oc = camera centre - centre and cc = |oc|^2 - r^2 in the group
 // record's pair-SoA form, (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1) per pair, evaluated in fp32

@@ -20,6 +20,8 @@
 // against fp32 emulations of the kernel's camera rays and discriminants.
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <limits>
 
 #include "cluster.hpp"
 #include "vcrt_math.h"
@@ -53,6 +55,19 @@ struct Pyramid {
     double n[4][3];  // inward side-plane normals
 };
 
+// No side plane separates the sphere (centre c, radius R) from the pyramid (conservative).
+bool sphere_outside(const Pyramid& P, const double c[3], double R) {
+    for (int k = 0; k < 4; k++) {
+        double s = 0.0, nn = 0.0;
+        for (int a = 0; a < 3; a++) {
+            s += P.n[k][a] * (c[a] - P.apex[a]);
+            nn += P.n[k][a] * P.n[k][a];
+        }
+        if (s + std::sqrt(nn) * R < 0.0) return true;
+    }
+    return false;
+}
+
 bool outside(const Pyramid& P, const DBox& b) {
     if (b.always) return false;
     for (int k = 0; k < 4; k++) {
@@ -68,41 +83,54 @@ bool outside(const Pyramid& P, const DBox& b) {
 
 }  // namespace
 
-void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
-                         int32_t height, int32_t rank, int32_t world, PrimaryLists& out) {
-    out.info.clear();
-    out.ids.clear();
-    const uint32_t tiles_x = static_cast<uint32_t>((width + 7) / 8);
-    const uint32_t tiles_y = static_cast<uint32_t>((height + 7) / 8);
+namespace {
+
+// The quarters of a rank's local tiles and, per quarter, the pyramid of its camera rays and the
+// hierarchy groups whose grown boxes it may meet (chunks, then their nodes, then their groups).
+struct QuarterWalker {
+    const CullTables& ct;
     double p00[3], du[3], dv[3], o[3];
-    for (int a = 0; a < 3; a++) {
-        p00[a] = cam[a];
-        du[a] = cam[3 + a];
-        dv[a] = cam[6 + a];
-        o[a] = cam[9 + a];
+    double ndu, ndv, Q;
+    uint32_t tiles_x, nloc;
+    int32_t rank, world;
+    std::vector<DBox> gb, nb, tb;
+    std::vector<bool> real;
+    static constexpr double kExtra = 1e-3;
+
+    QuarterWalker(const CullTables& c, const float cam[12], int32_t width, int32_t height,
+                  int32_t r, int32_t w)
+        : ct(c), rank(r), world(w) {
+        tiles_x = static_cast<uint32_t>((width + 7) / 8);
+        const uint32_t tiles_y = static_cast<uint32_t>((height + 7) / 8);
+        for (int a = 0; a < 3; a++) {
+            p00[a] = cam[a];
+            du[a] = cam[3 + a];
+            dv[a] = cam[6 + a];
+            o[a] = cam[9 + a];
+        }
+        const double on = std::sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
+        Q = (on + ct.margin[0]) * (on + ct.margin[0]) + ct.margin[1];
+        ndu = std::sqrt(du[0] * du[0] + du[1] * du[1] + du[2] * du[2]);
+        ndv = std::sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
+        const size_t ng = static_cast<size_t>(ct.ngroups);
+        gb.resize(ng);
+        nb.resize(ng / kNodeGroups);
+        tb.resize((ng + 63) / 64);
+        for (size_t i = 0; i < gb.size(); i++) gb[i] = grown_box(ct.bound, i, Q, kExtra);
+        for (size_t i = 0; i < nb.size(); i++) nb[i] = grown_box(ct.node, i, Q, kExtra);
+        for (size_t i = 0; i < tb.size(); i++) tb[i] = grown_box(ct.top, i, Q, kExtra);
+        real.assign(ng, false);
+        for (size_t i = 0; i < ng; i++)
+            for (int k = 0; k < 4; k++) real[i] = real[i] || ct.index[(ct.nbig + i) * 4 + k] >= 0;
+        // local tiles in the kernel's order (vcrt_math.h tile_of)
+        nloc = 0;
+        for (uint32_t ty = 0; ty < tiles_y; ty++)
+            for (uint32_t tx = 0; tx < tiles_x; tx++)
+                if ((tx + ty) % static_cast<uint32_t>(world) == static_cast<uint32_t>(rank)) nloc++;
     }
-    const double on = std::sqrt(o[0] * o[0] + o[1] * o[1] + o[2] * o[2]);
-    const double Q = (on + ct.margin[0]) * (on + ct.margin[0]) + ct.margin[1];
-    const double ndu = std::sqrt(du[0] * du[0] + du[1] * du[1] + du[2] * du[2]);
-    const double ndv = std::sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);
-    const double kExtra = 1e-3;
-    const size_t ng = static_cast<size_t>(ct.ngroups);
-    std::vector<DBox> gb(ng), nb(ng / kNodeGroups), tb((ng + 63) / 64);
-    for (size_t i = 0; i < gb.size(); i++) gb[i] = grown_box(ct.bound, i, Q, kExtra);
-    for (size_t i = 0; i < nb.size(); i++) nb[i] = grown_box(ct.node, i, Q, kExtra);
-    for (size_t i = 0; i < tb.size(); i++) tb[i] = grown_box(ct.top, i, Q, kExtra);
-    std::vector<bool> real(ng, false);
-    for (size_t i = 0; i < ng; i++)
-        for (int k = 0; k < 4; k++) real[i] = real[i] || ct.index[(ct.nbig + i) * 4 + k] >= 0;
-    // local tiles in the kernel's order (vcrt_math.h tile_of)
-    uint32_t nloc = 0;
-    for (uint32_t ty = 0; ty < tiles_y; ty++)
-        for (uint32_t tx = 0; tx < tiles_x; tx++)
-            if ((tx + ty) % static_cast<uint32_t>(world) == static_cast<uint32_t>(rank)) nloc++;
-    out.info.assign(4 * nloc, kPrimaryNone);
-    uint32_t found[kPrimaryMax];
-    for (uint32_t e = 0; e < 4 * nloc; e++) {
-        // entry 4 lt + 2 qy + qx: the 4x4-pixel quarter (qx, qy) of local tile lt
+
+    // entry e = 4 lt + 2 qy + qx: the 4x4-pixel quarter (qx, qy) of local tile lt
+    Pyramid pyramid(uint32_t e) const {
         const uint32_t lt = e >> 2, qx = e & 1u, qy = (e >> 1) & 1u;
         uint32_t tx, ty;
         tile_of(lt, static_cast<uint32_t>(rank), static_cast<uint32_t>(world), tiles_x, &tx, &ty);
@@ -127,26 +155,104 @@ void build_primary_lists(const CullTables& ct, const float cam[12], int32_t widt
             const double s = n[0] * mid[0] + n[1] * mid[1] + n[2] * mid[2];
             for (int a = 0; a < 3; a++) P.n[k][a] = s < 0.0 ? -n[a] : n[a];
         }
-        uint32_t cnt = 0;
-        bool over = false;
-        for (size_t ci = 0; ci < tb.size() && !over; ci++) {
+        return P;
+    }
+
+    // The groups the pyramid may meet, in hierarchy order; false when there are more than `cap`.
+    bool groups(const Pyramid& P, uint32_t cap, std::vector<uint32_t>& found) const {
+        found.clear();
+        for (size_t ci = 0; ci < tb.size(); ci++) {
             if (outside(P, tb[ci])) continue;
-            for (size_t ni = ci * 8; ni < std::min(nb.size(), ci * 8 + 8) && !over; ni++) {
+            for (size_t ni = ci * 8; ni < std::min(nb.size(), ci * 8 + 8); ni++) {
                 if (outside(P, nb[ni])) continue;
                 for (size_t gi = ni * kNodeGroups; gi < ni * kNodeGroups + kNodeGroups; gi++) {
                     if (!real[gi] || outside(P, gb[gi])) continue;
-                    if (cnt == kPrimaryMax) {
-                        over = true;
-                        break;
-                    }
-                    found[cnt++] = static_cast<uint32_t>(gi);
+                    if (found.size() == cap) return false;
+                    found.push_back(static_cast<uint32_t>(gi));
                 }
             }
         }
+        return true;
+    }
+};
+
+}  // namespace
+
+void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
+                         int32_t height, int32_t rank, int32_t world, PrimaryLists& out) {
+    out.info.clear();
+    out.ids.clear();
+    const QuarterWalker qw(ct, cam, width, height, rank, world);
+    const size_t ng = static_cast<size_t>(ct.ngroups);
+    out.info.assign(4 * qw.nloc, kPrimaryNone);
+    std::vector<uint32_t> found;
+    for (uint32_t e = 0; e < 4 * qw.nloc; e++) {
+        const bool fits = qw.groups(qw.pyramid(e), kPrimaryMax, found);
+        const size_t cnt = found.size();
         // ids are uint16 and offsets 28-bit: beyond that the quarter keeps no list
-        if (over || ng > 0xFFFFu || out.ids.size() + cnt >= (size_t{1} << 28)) continue;
-        out.info[e] = static_cast<uint32_t>(out.ids.size()) << 4 | cnt;
-        for (uint32_t k = 0; k < cnt; k++) out.ids.push_back(static_cast<uint16_t>(found[k]));
+        if (!fits || ng > 0xFFFFu || out.ids.size() + cnt >= (size_t{1} << 28)) continue;
+        out.info[e] = static_cast<uint32_t>(out.ids.size()) << 4 | static_cast<uint32_t>(cnt);
+        for (uint32_t g : found) out.ids.push_back(static_cast<uint16_t>(g));
+    }
+}
+
+void build_primary_sphere_lists(const CullTables& ct, const vcrt_sphere* spheres,
+                                const float cam[12], int32_t width, int32_t height, int32_t rank,
+                                int32_t world, PrimarySphereLists& out) {
+    out.info.clear();
+    out.rec.clear();
+    const QuarterWalker qw(ct, cam, width, height, rank, world);
+    out.info.assign(4 * qw.nloc, kPrimaryNone);
+    const float ox = cam[9], oy = cam[10], oz = cam[11];
+    std::vector<uint32_t> found;
+    std::vector<int32_t> members;
+    for (uint32_t e = 0; e < 4 * qw.nloc; e++) {
+        const Pyramid P = qw.pyramid(e);
+        // the group walk bounds the work; a quarter meeting very many groups keeps no list
+        if (!qw.groups(P, 64, found)) continue;
+        members.clear();
+        bool over = false;
+        for (uint32_t gi : found) {
+            for (int k = 0; k < 4 && !over; k++) {
+                const int32_t j = ct.index[(ct.nbig + gi) * 4 + k];
+                if (j < 0) continue;
+                const vcrt_sphere& sp = spheres[j];
+                const double c[3] = {sp.center[0], sp.center[1], sp.center[2]};
+                const double r = std::fabs(static_cast<double>(sp.radius));
+                double oc2 = 0.0;
+                for (int a = 0; a < 3; a++) oc2 += (qw.o[a] - c[a]) * (qw.o[a] - c[a]);
+                // the member's own margin (tracer.hip fact (2)), and the rounding of the rays
+                const double Ms = r > 0.0 ? 8.1 * 0x1p-24 * (oc2 + r * r) / r * (1.0 + 1e-5)
+                                          : std::numeric_limits<double>::infinity();
+                if (!(Ms < 1e30) || !sphere_outside(P, c, r + Ms + QuarterWalker::kExtra)) {
+                    if (members.size() == kPrimarySphereMax) over = true;
+                    else members.push_back(j);
+                }
+            }
+        }
+        if (over) continue;
+        const size_t first = out.rec.size() / 12;
+        if (first >= (size_t{1} << 28)) continue;
+        out.info[e] = static_cast<uint32_t>(first) << 4 | static_cast<uint32_t>(members.size());
+        for (size_t m = 0; m < members.size(); m += 2) {
+            float r[12] = {0, 0, 0, 0, 0, 0, 3.0e38f, 3.0e38f, 0, 0, 0, 0};
+            int32_t idx[2] = {-1, -1};
+            for (int e2 = 0; e2 < 2 && m + e2 < members.size(); e2++) {
+                const vcrt_sphere& sp = spheres[members[m + e2]];
+                // pair_disc_cc's operations and order: oc = o - c, cc = ((ocx ocx + ocy ocy) +
+                // ocz ocz) - r^2 with r^2 = radius * radius, fp32, no FMA
+                const float ocx = ox - sp.center[0], ocy = oy - sp.center[1],
+                            ocz = oz - sp.center[2];
+                const float r2 = sp.radius * sp.radius;
+                r[0 + e2] = ocx;
+                r[2 + e2] = ocy;
+                r[4 + e2] = ocz;
+                r[6 + e2] = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
+                idx[e2] = members[m + e2];
+            }
+            std::memcpy(&r[8], idx, sizeof(idx));
+            out.rec.insert(out.rec.end(), r, r + 12);
+        }
     }
 }
 

@@ -298,7 +298,7 @@ __device__ __forceinline__ void pair_disc_cc(const v2f ox, const v2f oy, const v
 }
 
 // pair_disc_cc for a camera ray (o = the camera centre) from the camera-relative record
-// (TraceParams.cam_oc: oc and cc as pair_disc_cc computes them for that o): the remaining
+// (TraceParams.cam_rec: oc and cc as pair_disc_cc computes them for that o): the remaining
 // operations, in the same order, on the same operands -- the same bits, at half the work.
 __device__ __forceinline__ void pair_disc_cam(const v2f dx, const v2f dy, const v2f dz,
                                               const v2f a2, float4 oxy, float4 ozc, v2f& hb,
@@ -948,7 +948,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     // the camera-ray list record, loaded ahead of the big list so its latency overlaps it
     uint32_t inf = 15u;
     if (primary && p.prim_info != nullptr)  // the list of the item's 4x4 quarter (slot 8 y + x)
-        inf = p.prim_info[(item >> 6) * 4u + (((item >> 5) & 1u) << 1) + ((item >> 2) & 1u)];
+        inf = p.prim_info[2u * ((item >> 6) * 4u + (((item >> 5) & 1u) << 1) + ((item >> 2) & 1u))];
     FlatRay my;
     my.ox = o.x;
     my.oy = o.y;
@@ -1263,6 +1263,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     uint32_t segs = 0;  // this lane's segments (< 2^32: ~2.4e5 per lane at the C5 workload)
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
     uint64_t w_groups = 0, w_bounds = 0;  // per wave (uniform): sphere groups / bounds tested
+    uint32_t w_pairs = 0;                 // per wave: sphere-pair tests of the camera lists
     PhaseTicks pt;                         // stats builds: wave clock per phase
     uint64_t t_begin = 0;
     if constexpr (kStats) t_begin = ticks();
@@ -1494,8 +1495,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             uint64_t t_cam = 0;
             if constexpr (kStats) t_cam = ticks();
             uint32_t inf = 15u;
-            if (fresh && p.prim_info != nullptr)  // the list of the item's 4x4 quarter
-                inf = p.prim_info[(q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)];
+            if (fresh && p.prim_info != nullptr)  // the sphere list of the item's 4x4 quarter
+                inf = p.prim_info[2u * ((q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)) +
+                                  1u];
             const float aa = dot(d, d);
             const bool cam_now = fresh && (inf & 15u) != 15u && (p.flags & kFlagSceneBounded) != 0 &&
                                  aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
@@ -1511,49 +1513,44 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 uint32_t iters = 0, roots = 0;
                 if (cam_now) {
                     ++segs;
-                    // A camera ray starts at the camera centre: its members' oc and cc come
-                    // from the camera-relative records (pair_disc_cam: same bits, half the
-                    // arithmetic of pair_disc_cc); the roots take candidate_t_fast.
-                    cfloat4* crec = (cfloat4*)p.cam_oc;
+                    // A camera ray starts at the camera centre: its spheres' oc and cc come from
+                    // camera-relative records (pair_disc_cam: same bits, half the arithmetic of
+                    // pair_disc_cc); the roots take candidate_t_fast.
+                    cfloat4* crec = (cfloat4*)p.cam_rec;
                     const float ya = recip_a(aa);
                     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
                     for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres (scalar loads)
                         exact_group_uniform_cam(crec + 4 * gb, (cfloat4*)p.cgroup + 5 * gb, dx, dy,
                                                 dz, a2, aa, ya, mt, bst);
+                    // the quarter's listed spheres, two per record (primary.cpp): the exact
+                    // test's may-hit bits are collected first (bit 2k + s)...
                     const uint32_t cnt = inf & 15u;
-                    const uint16_t* ids = p.prim_ids + (inf >> 4);
-                    // the listed groups: the exact test of the four members, whose may-hit
-                    // bits are collected (bit 4k + s)...
+                    const float4* lr = p.cam_rec + 4u * (uint32_t)p.nbig + 3u * (inf >> 4);
                     uint32_t cbits = 0u;
-                    for (uint32_t k = 0; k < cnt; ++k) {
+                    for (uint32_t k = 0; 2u * k < cnt; ++k) {
                         ++iters;
-                        const float4* c = p.cam_oc + 4u * ((uint32_t)p.nbig + ids[k]);
-                        const float4 q0 = c[0], q1 = c[1], q2 = c[2], q3 = c[3];
-                        v2f hb01, cc01, d01, hb23, cc23, d23;
-                        pair_disc_cam(dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
-                        pair_disc_cam(dx, dy, dz, a2, q2, q3, hb23, cc23, d23);
-                        uint32_t hits = push_sign(0u, hit_sign(hb23.y, cc23.y, d23.y));
-                        hits = push_sign(hits, hit_sign(hb23.x, cc23.x, d23.x));
-                        hits = push_sign(hits, hit_sign(hb01.y, cc01.y, d01.y));
-                        hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
-                        cbits |= hits << (4u * k);
+                        const float4 q0 = lr[3u * k], q1 = lr[3u * k + 1u];
+                        v2f hb, cc, dc;
+                        pair_disc_cam(dx, dy, dz, a2, q0, q1, hb, cc, dc);
+                        const uint32_t hits = push_sign(push_sign(0u, hit_sign(hb.y, cc.y, dc.y)),
+                                                        hit_sign(hb.x, cc.x, dc.x));
+                        cbits |= hits << (2u * k);
                     }
                     // ...then the candidates' roots, one per lane and loop trip (the wave runs
                     // as many trips as its busiest lane has candidates, mostly one), with the
-                    // member's hb and disc recomputed by the same operations
+                    // sphere's hb and disc recomputed by the same operations
                     while (cbits) {
                         const uint32_t b = (uint32_t)__builtin_ctz(cbits);
                         cbits &= cbits - 1u;
-                        const uint32_t sm = b & 3u;
-                        const uint32_t gi = ids[b >> 2];
-                        const float4* c = p.cam_oc + 4u * ((uint32_t)p.nbig + gi);
-                        const float4 xy = c[(sm >> 1) * 2], zc = c[(sm >> 1) * 2 + 1];
-                        const bool hi = (sm & 1u) != 0;
+                        const float4* c = lr + 3u * (b >> 1);
+                        const float4 xy = c[0], zc = c[1], id = c[2];
+                        const bool hi = (b & 1u) != 0;
                         const float ocx = hi ? xy.y : xy.x, ocy = hi ? xy.w : xy.z;
                         const float ocz = hi ? zc.y : zc.x, cc = hi ? zc.w : zc.z;
                         const float hb = ocx * d.x + ocy * d.y + ocz * d.z;
                         const float disc = hb * hb - aa * cc;
-                        consider(candidate_t_fast(hb, disc, aa, ya), tg.index(gi, sm), mt, bst);
+                        consider(candidate_t_fast(hb, disc, aa, ya),
+                                 __float_as_int(hi ? id.y : id.x), mt, bst);
                         ++roots;
                     }
                 }
@@ -1570,8 +1567,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     pt.list_trips += ml;
                     pt.root_trips += mr;
                 }
-                // issued work: the big list and the loop's passes, per wave
-                w_groups += (uint64_t)p.nbig + wave_max_small<4>(iters);
+                // issued work: the big list and the loop's passes (a pair test is half a group
+                // test), per wave
+                w_groups += (uint64_t)p.nbig;
+                w_pairs += wave_max_small<3>(iters);
             }
             // One shading for the camera rays just traced and the main-scan hits of the last
             // iteration: the hit branches run once per iteration for both (a lane has at most
@@ -1667,7 +1666,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
     if (lane == 0 && total) atomicAdd(p.segments, total);
     if (lane == 0 && p.work_done) {
-        atomicAdd(p.work_done + 0, (unsigned long long)w_groups);
+        atomicAdd(p.work_done + 0, (unsigned long long)(w_groups + w_pairs / 2u));
         atomicAdd(p.work_done + 1, (unsigned long long)w_bounds);
     }
     if constexpr (kStats) {

@@ -49,14 +49,19 @@ struct TraceParams {
     const float4* cnode_nf;  // [ceil(ncgroups / 64) * 4 * 5] the node-pair boxes in the near/far
                              //   layout of cbound_nf, padded to whole chunks (the flat scan's
                              //   chunk passes)
-    const uint32_t* prim_info;  // [4 local_tiles] camera-ray group list of each 4x4 quarter
-                                //   (4 lt + 2 qy + qx) of each local tile: offset << 4 |
-                                //   count (count <= 8; 15 = none), or null
-    const uint16_t* prim_ids;   // hierarchy group indices of those lists
-    const float4* cam_oc;       // [(nbig + ncgroups) * 4] with the lists: per group the members'
-                                //   oc = camera centre - centre and cc = |oc|^2 - r^2, pair-SoA
-                                //   (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1) (..2,3..), fp32 as
-                                //   pair_disc_cc computes them (cluster.hpp build_camera_records)
+    const uint32_t* prim_info;  // [4 local_tiles][2] camera-ray lists of each 4x4 quarter
+                                //   (4 lt + 2 qy + qx) of each local tile, or null: [0] the
+                                //   hierarchy groups (main scan) as offset << 4 | count (<= 8),
+                                //   [1] the spheres (camera fast trace) as first pair << 4 |
+                                //   count (<= 14); 15 = no list
+    const uint16_t* prim_ids;   // hierarchy group indices of the group lists
+    const float4* cam_rec;      // with the lists: [nbig * 4] the big groups' camera-relative
+                                //   records, pair-SoA (ocx0,ocx1,ocy0,ocy1) (ocz0,ocz1,cc0,cc1)
+                                //   (..2,3..) with oc = camera centre - centre, cc = |oc|^2 - r^2,
+                                //   fp32 as pair_disc_cc computes them; then the sphere lists'
+                                //   pair records [pairs * 3]: (ocx0,ocx1,ocy0,ocy1)
+                                //   (ocz0,ocz1,cc0,cc1) (index0, index1 as int bits, 0, 0)
+                                //   (cluster.hpp build_camera_records / build_primary_sphere_lists)
     float box_margin[4];    // max |centre|, r_max^2, max |box coordinate|, 0 (rounded up)
     int32_t ncgroups;       // hierarchy groups, multiple of 16
     int32_t nbig;           // big-sphere groups tested for every ray

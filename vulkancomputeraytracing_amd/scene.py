@@ -112,3 +112,25 @@ def primary_lists(spheres: np.ndarray, desc) -> dict | None:
                                  info.ctypes.data, nt, ids.ctypes.data, len(ids))
     assert got == n
     return {"info": info, "ids": ids[:n]}
+
+
+def primary_sphere_lists(spheres: np.ndarray, desc) -> dict | None:
+    """The camera fast trace's per-sphere lists (host computation, no GPU; csrc/primary.cpp):
+    ``info`` [4 x local tiles] uint32 (first pair << 4 | spheres, 15 = no list) and ``rec``
+    [pairs, 12] float32 camera-relative pair records (ocx0 ocx1 ocy0 ocy1 ocz0 ocz1 cc0 cc1
+    index0 index1 0 0, the indices as int32 bits). None without culling tables."""
+    spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+    lib = N.lib()
+    d = desc.to_c()
+    n = lib.vcrt_primary_sphere_lists(spheres.ctypes.data, len(spheres), ctypes.byref(d), None,
+                                      0, None, 0)
+    if n < 0:
+        return None
+    from .renderer import tiles_for_rank
+    nt = 4 * len(tiles_for_rank(desc.width, desc.height, desc.world_size, desc.rank))
+    info = np.zeros(nt, np.uint32)
+    rec = np.zeros((max(n, 1), 12), np.float32)
+    got = lib.vcrt_primary_sphere_lists(spheres.ctypes.data, len(spheres), ctypes.byref(d),
+                                        info.ctypes.data, nt, rec.ctypes.data, rec.size)
+    assert got == n
+    return {"info": info, "rec": rec[:n]}
