@@ -132,7 +132,8 @@ typedef struct vcrt_stats {
     int32_t nspheres;
     uint32_t lds_bytes;
     int32_t accumulate_chunk; /* samples per work item in effect */
-    int32_t tables_in_lds;    /* 1 when the culled scan reads its tables from LDS */
+    int32_t tables_in_lds;    /* 1 when the culled scan reads its tables from LDS, 2 when only
+                                 its boxes (vcrt_trace_cull_flat_boxes) */
     uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
     uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
     uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */

@@ -200,14 +200,59 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
         assert st["tables_in_lds"]
     elif st["lds_bytes"] > 0:  # 114 KB: one copy per 1024-thread workgroup
         assert st["lds_bytes"] > 32768 and st["block_threads"] == 1024
-    # the flat scan: tables beside its stacks in LDS up to 32 KB, else in global memory
+    # the flat scan: tables beside its stacks in LDS up to 32 KB, else the boxes alone in LDS
+    # (up to 1024 groups), else everything in global memory
     got, st = gpu_render(scene, w, h, spp, depth, vc.KERNEL_CULL_FLAT)
     assert st["kernel_variant"] == vc.KERNEL_CULL_FLAT
     assert_bitwise(got, want, f"{scene} flat tables={tables}")
     assert st["segments"] == segs
-    assert st["tables_in_lds"] == (tables == "lds" and scene == "final")
-    if not st["tables_in_lds"]:
+    if tables == "global":
+        assert st["tables_in_lds"] == 0
         assert st["lds_bytes"] == 4 * 6912 and st["block_threads"] == 256
+    elif scene == "final":
+        assert st["tables_in_lds"] == 1 and st["block_threads"] == 256
+    else:
+        assert st["tables_in_lds"] == 2 and st["block_threads"] == 1024
+        assert st["kernel"] == "vcrt_trace_cull_flat_boxes"
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk", [
+    ("final", 40, 24, 3, 12, 0),
+    ("stress4096", 48, 27, 4, 50, 0),
+    ("stress4096", 37, 19, 6, 10, 4),
+    ("random3000", 40, 24, 2, 8, 0),
+    ("random9000", 40, 24, 2, 8, 0),
+    ("torture", 33, 21, 5, 50, 5),
+])
+def test_flat_scan_boxes_in_lds(oracle, monkeypatch, scene, w, h, spp, depth, chunk):
+    """The flat scan with only the boxes in LDS (1024-thread workgroups, group records from
+    global memory, 16-bit stacks): bit-identical to the oracle; scenes beyond 1024 hierarchy
+    groups fall back to the global-table kernel."""
+    monkeypatch.setenv("VCRT_CULL_LANE_TABLES", "boxes")
+    cfg = {}
+    if scene.startswith("random"):
+        n = int(scene[6:])
+        sc = random_large_scene(n, seed=n)
+        cfg = dict(lookfrom=(-80, 10, 5), lookat=(0, 0, 0), vfov=50)
+    elif scene == "torture":
+        sc = culling_torture_scene()
+    else:
+        sc = scene
+    k = chunk_of(w, h, spp, chunk)
+    oscene = oracle.scene(sc) if isinstance(sc, str) else sc
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **k, **cfg), oscene)
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         kernel_variant=vc.KERNEL_CULL_FLAT, accumulate_chunk=chunk, **cfg)
+    with vc.Renderer(desc, sc) as r:
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    assert_bitwise(got, want, f"{scene} flat boxes")
+    assert st["segments"] == segs
+    if scene == "random9000":  # 2250 groups: beyond the 16-bit entries
+        assert st["kernel"] == "vcrt_trace_cull_flat_global"
+    else:
+        assert st["kernel"] == "vcrt_trace_cull_flat_boxes"
+        assert st["block_threads"] == 1024 and st["lds_bytes"] > 16 * 4352
 
 
 def culling_torture_scene():
@@ -261,8 +306,9 @@ def test_large_random_scene_all_variants(oracle, n):
             r.draw_next_frame()
             got, st = r.read_framebuffer(), r.stats()
         assert st["kernel_variant"] == variant and st["nspheres"] == n
-        if variant == vc.KERNEL_CULL_FLAT:  # tables beyond LDS: the global-table flat kernel
-            assert not st["tables_in_lds"]
+        if variant == vc.KERNEL_CULL_FLAT:  # tables beyond 32 KB: boxes only in LDS (up to
+            # 1024 groups), else the global-table flat kernel
+            assert st["tables_in_lds"] == (2 if n <= 4096 else 0)
         assert_bitwise(got, want, f"random {n} v{variant}")
         assert st["segments"] == segs
 
@@ -637,7 +683,7 @@ def test_camera_ray_lists_switch_keeps_bits(monkeypatch):
 @pytest.mark.parametrize("scene,variant,kernel", [
     ("final", vc.KERNEL_AUTO, "vcrt_trace_cull_flat"),
     ("three", vc.KERNEL_AUTO, "vcrt_trace_smem"),
-    ("stress4096", vc.KERNEL_AUTO, "vcrt_trace_cull_flat_global"),
+    ("stress4096", vc.KERNEL_AUTO, "vcrt_trace_cull_flat_boxes"),
     ("final", vc.KERNEL_LDS, "vcrt_trace_lds"),
     ("final", vc.KERNEL_CULL, "vcrt_trace_cull"),
     ("final", vc.KERNEL_CULL_LANE, "vcrt_trace_cull_lane_lds"),

@@ -54,8 +54,10 @@ struct RendererState {
                   k_trace_cull_lane_stats = nullptr, k_trace_cull_lane_lds_wide = nullptr,
                   k_trace_cull_lane_lds_wide_stats = nullptr, k_trace_cull_flat = nullptr,
                   k_trace_cull_flat_stats = nullptr, k_trace_cull_flat_global = nullptr,
-                  k_trace_cull_flat_global_stats = nullptr;
-    int cull_lane_tables = 0;  // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global
+                  k_trace_cull_flat_global_stats = nullptr, k_trace_cull_flat_boxes = nullptr,
+                  k_trace_cull_flat_boxes_stats = nullptr;
+    // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global, 3 = boxes in LDS (flat scan)
+    int cull_lane_tables = 0;
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     int debug_stats = 0;  // 1: the stats kernels; 2: the product kernels with a debug buffer
                           //    (builds with VCRT_WAVE_END_TIMES record wave start/end times)
@@ -336,6 +338,14 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_global, m, "vcrt_trace_cull_flat_global"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_global_stats, m,
                                   "vcrt_trace_cull_flat_global_stats"));
+    // optional: code objects built before the boxes-in-LDS flat scan lack it (A/B builds)
+    if (hipModuleGetFunction(&g.k_trace_cull_flat_boxes, m, "vcrt_trace_cull_flat_boxes") !=
+            hipSuccess ||
+        hipModuleGetFunction(&g.k_trace_cull_flat_boxes_stats, m,
+                             "vcrt_trace_cull_flat_boxes_stats") != hipSuccess) {
+        (void)hipGetLastError();
+        g.k_trace_cull_flat_boxes = g.k_trace_cull_flat_boxes_stats = nullptr;
+    }
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide, m,
                                   "vcrt_trace_cull_lane_lds_wide"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide_stats, m,
@@ -545,10 +555,20 @@ KernelChoice select_kernel() {
         variant = VCRT_KERNEL_SMEM;
     // The flat scan keeps 4.25 KB of stacks per wave in LDS beside its tables when they fit
     // in 32 KB (16-bit entries), in 256-thread workgroups (five per CU, each with its copy of
-    // the tables). Otherwise the tables stay in global memory and the stacks take 32-bit
-    // entries (6.75 KB per wave).
+    // the tables). Up to 1024 groups (16-bit entries) it keeps only the boxes in LDS, one copy
+    // per 1024-thread workgroup; beyond that the tables stay in global memory and the stacks
+    // take 32-bit entries (6.75 KB per wave).
     const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
-                          g.ncgroups <= vcrt::kFlatMaxGroups;
+                          g.cull_lane_tables != 3 && g.ncgroups <= vcrt::kFlatMaxGroups;
+    // Boxes only (near/far group boxes + node boxes of whole chunks) in LDS, one copy for the
+    // 16 waves of a 1024-thread workgroup, beside their 16-bit stacks; the records from global.
+    const uint32_t box_lds = static_cast<uint32_t>(
+        16 * (g.ncgroups / 2 * 5 + (g.ncgroups + 63) / 64 * 20) + 16 * vcrt::kWaveScratchBytes);
+    // Measured at C5 (stress scene, 4K, 4096 spp, depth 50): 11415 against 11186 Msamples/s
+    // with every table in global memory (same bits; profiles/r03_c5_boxes_*).
+    const bool flat_boxes = !flat_lds && g.k_trace_cull_flat_boxes != nullptr &&
+                            g.cull_lane_tables != 2 && g.ncgroups <= vcrt::kFlatMaxGroups &&
+                            box_lds <= g.max_lds;
     hipFunction_t f = g.k_trace_smem, fs = g.k_trace_smem_stats;
     const char* fname = "vcrt_trace_smem";
     uint32_t block = 256;
@@ -567,6 +587,12 @@ KernelChoice select_kernel() {
         fs = g.k_trace_cull_flat_stats;
         fname = "vcrt_trace_cull_flat";
         lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
+    } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_boxes) {
+        f = g.k_trace_cull_flat_boxes;
+        fs = g.k_trace_cull_flat_boxes_stats;
+        fname = "vcrt_trace_cull_flat_boxes";
+        block = 1024;
+        lds = box_lds;
     } else if (variant == VCRT_KERNEL_CULL_FLAT) {
         f = g.k_trace_cull_flat_global;
         fs = g.k_trace_cull_flat_global_stats;
@@ -739,7 +765,10 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e);
     if (const char* e = std::getenv("VCRT_PRIMARY_LISTS")) g.primary_lists = std::atoi(e) != 0;
     if (const char* e = std::getenv("VCRT_CULL_LANE_TABLES"))
-        g.cull_lane_tables = std::strcmp(e, "lds") == 0 ? 1 : std::strcmp(e, "global") == 0 ? 2 : 0;
+        g.cull_lane_tables = std::strcmp(e, "lds") == 0      ? 1
+                             : std::strcmp(e, "global") == 0 ? 2
+                             : std::strcmp(e, "boxes") == 0  ? 3
+                                                             : 0;
     // Blocks run from the last local tile to the first: the bottom of the frame (ground and
     // spheres, many bounces) first, the sky last, which shortens the drain at the end of the
     // queue (N = 8: 34.8 -> 33.8 ms per rank). VCRT_WORK_ORDER=forward restores top-down.
@@ -1045,8 +1074,9 @@ vcrt_result vcrt_draw_next_frame(void) {
         g.stats.block_threads = static_cast<int32_t>(block);
         g.stats.kernel_variant = variant;
         g.stats.lds_bytes = lds;
-        g.stats.tables_in_lds = (f == g.k_trace_cull_flat || f == g.k_trace_cull_lane_lds ||
-                                 f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
+        g.stats.tables_in_lds = kc.f == g.k_trace_cull_flat_boxes ? 2 :
+                                (kc.f == g.k_trace_cull_flat || kc.f == g.k_trace_cull_lane_lds ||
+                                 kc.f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
     }
     if (g.comm && g.desc.world_size > 1) {
         VkResult r = gather_frame();

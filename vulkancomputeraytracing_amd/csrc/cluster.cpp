@@ -147,6 +147,21 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
         big.resize(64);
         std::sort(big.begin(), big.end());
     }
+    // The flat scans' 16-bit stack entries address up to kFlatGroups16 hierarchy groups. When the
+    // hierarchy would exceed that by no more than the free slots of the big list's last group
+    // (the stress scene: 4096 random spheres + the big three), the largest of the rest fill
+    // those slots (ties by index): every ray tests them anyway as part of that group.
+    const size_t free_slots = (4 - big.size() % 4) % 4;
+    if (!big.empty() && normal.size() > 4 * kFlatGroups16 &&
+        normal.size() - 4 * kFlatGroups16 <= free_slots) {
+        std::stable_sort(normal.begin(), normal.end(),
+                         [&](int32_t x, int32_t y) { return radii[x] > radii[y]; });
+        const size_t move = normal.size() - 4 * kFlatGroups16;
+        big.insert(big.end(), normal.begin(), normal.begin() + move);
+        normal.erase(normal.begin(), normal.begin() + move);
+        std::sort(big.begin(), big.end());
+        std::sort(normal.begin(), normal.end());
+    }
     // Big spheres go to a short list the kernels test for every ray (they are hit by most);
     // the rest form the hierarchy: groups of 4, nodes of 8 groups, chunks of 64 groups.
     std::vector<Group> bigg, groups;

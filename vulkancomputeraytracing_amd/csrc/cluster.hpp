@@ -15,6 +15,7 @@
 namespace vcrt {
 
 constexpr int kNodeGroups = 8;  // groups per node of the box hierarchy
+constexpr size_t kFlatGroups16 = 1024;  // = vcrt::kFlatMaxGroups (10-bit entry fields)
 
 struct CullTables {
     int32_t nbig = 0;             // big-sphere groups, first in geom/index, tested for every ray

@@ -671,19 +671,19 @@ struct WaveScratch {
 static_assert(sizeof(WaveScratch<false>) == kWaveScratchBytes, "host LDS size");
 static_assert(sizeof(WaveScratch<true>) == kWaveScratchBytesWide, "host LDS size");
 
-// The flat scans' hierarchy group records. Global tables (kWide): the 80-B records of
+// The flat scans' hierarchy group records. Global records (kGRec): the 80-B records of
 // TraceParams.cgroup (four pair-SoA float4s + the members' world[] indices as int bits). LDS
-// tables: the four float4s (64 B per group) and the indices as uint16 in a table of their own
+// records: the four float4s (64 B per group) and the indices as uint16 in a table of their own
 // (8 B per group): 1 KB less LDS per workgroup for the final scene's 128 groups.
-template <bool kWide>
+template <bool kGRec>
 struct GroupTab {
     const float4* geom;
     const uint16_t* idx;  // LDS layout only
     __device__ __forceinline__ const float4* rec(uint32_t gi) const {
-        return geom + (kWide ? 5u : 4u) * gi;
+        return geom + (kGRec ? 5u : 4u) * gi;
     }
     __device__ __forceinline__ int index(uint32_t gi, uint32_t s) const {
-        if constexpr (kWide) {
+        if constexpr (kGRec) {
             const float4 idf = geom[5u * gi + 4u];
             return __float_as_int(s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w);
         } else {
@@ -749,11 +749,11 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 // 1: group, 2: node. Lanes ranked past the entries run on their own ray and push nothing.
 // kKind 0: cand, 1: group, 2: node. n: this stack's height; pushed: the height of the stack
 // this pass pushes onto (group for node passes, cand for group passes).
-template <int kKind, bool kWide>
+template <int kKind, bool kWide, bool kGRec>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
                                           uint32_t rank, uint32_t lane, WaveScratch<kWide>* ws,
                                           const float4* tbound, const float4* tnode, uint32_t ncg,
-                                          const GroupTab<kWide>& tg, const FlatRay& my) {
+                                          const GroupTab<kGRec>& tg, const FlatRay& my) {
     using F = FlatFmt<kWide>;
     using entry_t = typename F::entry_t;
     const uint32_t m = min(n, nact), top = n - m;
@@ -874,11 +874,11 @@ struct FlatStacks {  // wave-uniform stack heights
     uint32_t cand, group, node, chunk;
 };
 
-template <bool kStats, bool kWide>
+template <bool kStats, bool kWide, bool kGRec>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
                                            WaveScratch<kWide>* ws, FlatStacks& h,
                                            const float4* tbound, const float4* tnode, uint32_t ncg,
-                                           const GroupTab<kWide>& tg, const FlatRay& my,
+                                           const GroupTab<kGRec>& tg, const FlatRay& my,
                                            uint32_t& n_groups, uint32_t& n_bounds,
                                            PhaseTicks& pt) {
     uint32_t nc = h.cand, ng = h.group, nn = h.node, nk = h.chunk;
@@ -909,22 +909,22 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         else if (nk >= nact) kind = 3;
         else if (th == 1u) kind = nk ? 3 : nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
-            flat_pass<0, kWide>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<0, kWide, kGRec>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (kind == 1) {
             ++n_groups;
-            flat_pass<1, kWide>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<1, kWide, kGRec>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
             n_bounds += 8;
-            flat_pass<2, kWide>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<2, kWide, kGRec>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else if (kind == 3) {
             n_bounds += 8;
-            flat_pass<3, kWide>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<3, kWide, kGRec>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.levels += ticks() - t0;
         } else {
             break;
@@ -936,9 +936,13 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
     h.chunk = nk;
 }
 
-template <bool kStats, bool kWide>
+// kChunks: the chunk level as per-lane chunk passes over the near/far node boxes `tnode` (many
+// chunks: the stress scene), else wave-uniform node tests on scalar-loaded boxes (two chunks:
+// the final scene).
+template <bool kStats, bool kWide, bool kGRec, bool kChunks>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
-                                                 const GroupTab<kWide>& tg, WaveScratch<kWide>* ws,
+                                                 const float4* tnode,
+                                                 const GroupTab<kGRec>& tg, WaveScratch<kWide>* ws,
                                                  const f3 o, const f3 d, bool primary,
                                                  uint32_t item, float& max_t, int& best,
                                                  uint64_t& groups_tested, uint64_t& bounds_tested,
@@ -1011,9 +1015,9 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             const bool in_chunk = !listed && ((tops >> ((base >> 6) & 1)) & 1u) != 0;
             const uint64_t want = __ballot(in_chunk);
             if (want == 0) continue;
-            if constexpr (kWide) {
-            // level 1 (global tables: many chunks): a chunk entry per lane whose ray may meet
-            // the chunk; chunk passes test its nodes for that lane alone
+            if constexpr (kChunks) {
+            // level 1 (many chunks): a chunk entry per lane whose ray may meet the chunk; chunk
+            // passes test its nodes for that lane alone
             if (in_chunk)
                 ws->chunk[h.chunk + lanes_below(want)] = (typename FlatFmt<kWide>::entry_t)(
                     (lane << FlatFmt<kWide>::kShift) | ((uint32_t)base >> 6));
@@ -1052,8 +1056,8 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             if constexpr (kStats) pt.push += ticks() - t0;
             }
         }
-        flat_drain<kStats, kWide>(th, nact, rank, lane, ws, h, tbound, p.cnode_nf,
-                                  (uint32_t)ncg, tg, my, n_groups, n_bounds, pt);
+        flat_drain<kStats, kWide, kGRec>(th, nact, rank, lane, ws, h, tbound, tnode,
+                                         (uint32_t)ncg, tg, my, n_groups, n_bounds, pt);
         if (base >= ncg) break;
     }
     __builtin_amdgcn_wave_barrier();
@@ -1199,14 +1203,18 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     }
     // group-pair boxes: the flat scan reads the near/far layout (80 B per pair), the others
     // the pair-SoA one (64 B)
-    constexpr bool kNearFar = kCull == 4 || kCull == 5;
-    const float4* tbound = kNearFar ? p.cbound_nf : p.cbound;
+    constexpr bool kFlat = kCull == 4 || kCull == 5 || kCull == 6;
+    const float4* tbound = kFlat ? p.cbound_nf : p.cbound;
+    const float4* tnode = p.cnode_nf;              // the flat scans' chunk passes
     const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
-    // the flat scan's stacks: after the LDS tables (kCull 4), or alone with the tables in
-    // global memory and 32-bit entries (kCull 5)
+    // the flat scan's stacks: after the LDS tables (kCull 4: all tables; kCull 6: the boxes,
+    // with the group records in global memory), or alone with the tables in global memory and
+    // 32-bit entries (kCull 5)
     constexpr bool kWide = kCull == 5;
+    constexpr bool kGRec = kCull == 5 || kCull == 6;
+    constexpr bool kChunks = kCull == 5 || kCull == 6;
     WaveScratch<kWide>* ws = nullptr;
-    GroupTab<kWide> tg{tgroup, nullptr};  // the flat scans' view of the group records
+    GroupTab<kGRec> tg{tgroup, nullptr};  // the flat scans' view of the group records
     if constexpr (kCull == 2) {
         const int nb = (p.ncgroups >> 1) * 4, ng = p.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
@@ -1236,6 +1244,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
              (threadIdx.x >> 6);
     }
     if constexpr (kCull == 5) ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom) + (threadIdx.x >> 6);
+    if constexpr (kCull == 6) {  // LDS: near/far group boxes, near/far node boxes (whole chunks)
+        const int nb = (p.ncgroups >> 1) * 5, nn = ((p.ncgroups + 63) >> 6) * 20;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
+        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds_geom[nb + i] = tnode[i];
+        __syncthreads();
+        tbound = lds_geom;
+        tnode = lds_geom + nb;
+        ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + nn) + (threadIdx.x >> 6);
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const f3 p00 = mk(p.cam[0], p.cam[1], p.cam[2]);
     const f3 du = mk(p.cam[3], p.cam[4], p.cam[5]);
@@ -1491,7 +1508,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         //      and t as the flat scan), and shaded; the lane then takes its first bounce
         //      through this iteration's scan. The per-wave costs of an iteration (uniform
         //      levels, ray setup, block fetch) are so shared by two segments of such lanes. ----
-        if constexpr (kCull == 4 || kCull == 5) {
+        if constexpr (kFlat) {
             uint64_t t_cam = 0;
             if constexpr (kStats) t_cam = ticks();
             uint32_t inf = 15u;
@@ -1604,9 +1621,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 if constexpr (kCull == 1)
                     scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
-                else if constexpr (kCull == 4 || kCull == 5)
-                    scan_culled_flat<kStats, kWide>(p, tbound, tg, ws, o, d, pass == 0, q,
-                                                    max_t, best, w_groups, w_bounds, pt);
+                else if constexpr (kFlat)
+                    scan_culled_flat<kStats, kWide, kGRec, kChunks>(
+                        p, tbound, tnode, tg, ws, o, d, pass == 0, q, max_t, best, w_groups,
+                        w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);
@@ -1632,7 +1650,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             t_shade = ticks();
             pt.shade_hits += (uint64_t)__popcll(__ballot(best >= 0));
         }
-        if constexpr (kCull == 4 || kCull == 5) {
+        if constexpr (kFlat) {
             if (best >= 0) {  // a hit: shaded with the next iteration's camera rays
                 pend_t = max_t;
                 pend_best = best;
@@ -1777,6 +1795,19 @@ __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_global_stats(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, true, 5>(p, lds_tab);
+}
+
+// The flat scan for up to 1024 hierarchy groups whose records do not fit in LDS beside the
+// stacks (the stress scene): the group and node boxes in LDS, one copy per CU for 16 waves
+// (1024-thread workgroups), the group records in global memory, 16-bit stack entries.
+extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 6>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes_stats(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, true, 6>(p, lds_tab);
 }
 
 #endif
