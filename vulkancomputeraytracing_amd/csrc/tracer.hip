@@ -1193,20 +1193,30 @@ __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, ui
 // kCull: 0 = linear scan (kLds: table in LDS), 1 = culled scan, 2 = per-lane culled scan
 // with the group tables copied to LDS, 3 = per-lane culled scan on global tables.
 template <bool kLds, bool kStats, int kCull = 0>
-__device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn) {
-    const int n = p.nspheres;
+__device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds_dyn) {
+    // P: the kernel arguments, read through a pointer to the kernarg segment (the kernels' only
+    // argument) that the persistent loop makes opaque at the top of every iteration (below), so
+    // that the compiler re-reads the arguments it needs (scalar loads from the constant cache)
+    // instead of keeping every value derived from them live across the loop. That freed the ~75
+    // SGPRs the flat kernel spilled to VGPR lanes (a v_readlane per reload): C4 +2.6%, stress
+    // scene +5%, same bits.
+    (void)p_arg;
+    const TraceParams* pargs = reinterpret_cast<const TraceParams*>(
+        (__attribute__((address_space(4))) const TraceParams*)__builtin_amdgcn_kernarg_segment_ptr());
+#define P (*pargs)
+    const int n = P.nspheres;
     float4* const lds_geom = lds_dyn;
     if constexpr (kLds) {
         const int nq = 4 * (((n + 3) >> 2) + 1);
-        for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = p.geom[i];
+        for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = P.geom[i];
         __syncthreads();
     }
     // group-pair boxes: the flat scan reads the near/far layout (80 B per pair), the others
     // the pair-SoA one (64 B)
     constexpr bool kFlat = kCull == 4 || kCull == 5 || kCull == 6;
-    const float4* tbound = kFlat ? p.cbound_nf : p.cbound;
-    const float4* tnode = p.cnode_nf;              // the flat scans' chunk passes
-    const float4* tgroup = p.cgroup + 5 * p.nbig;  // the hierarchy's group records
+    const float4* tbound = kFlat ? P.cbound_nf : P.cbound;
+    const float4* tnode = P.cnode_nf;              // the flat scans' chunk passes
+    const float4* tgroup = P.cgroup + 5 * P.nbig;  // the hierarchy's group records
     // the flat scan's stacks: after the LDS tables (kCull 4: all tables; kCull 6: the boxes,
     // with the group records in global memory), or alone with the tables in global memory and
     // 32-bit entries (kCull 5)
@@ -1216,7 +1226,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     WaveScratch<kWide>* ws = nullptr;
     GroupTab<kGRec> tg{tgroup, nullptr};  // the flat scans' view of the group records
     if constexpr (kCull == 2) {
-        const int nb = (p.ncgroups >> 1) * 4, ng = p.ncgroups * 5;
+        const int nb = (P.ncgroups >> 1) * 4, ng = P.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) lds_geom[nb + i] = tgroup[i];
         __syncthreads();
@@ -1224,12 +1234,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         tgroup = lds_geom + nb;
     }
     if constexpr (kCull == 4) {  // LDS: near/far boxes, 64-B group records, uint16 indices
-        const int nb = (p.ncgroups >> 1) * 5, ng = p.ncgroups * 4;
+        const int nb = (P.ncgroups >> 1) * 5, ng = P.ncgroups * 4;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
         for (int i = threadIdx.x; i < ng; i += blockDim.x)
             lds_geom[nb + i] = tgroup[5 * (i >> 2) + (i & 3)];
         uint16_t* idx = reinterpret_cast<uint16_t*>(lds_geom + nb + ng);
-        for (int i = threadIdx.x; i < p.ncgroups; i += blockDim.x) {
+        for (int i = threadIdx.x; i < P.ncgroups; i += blockDim.x) {
             const float4 idf = tgroup[5 * i + 4];  // member indices < 2^16 (<= 1024 groups)
             idx[4 * i + 0] = (uint16_t)__float_as_int(idf.x);
             idx[4 * i + 1] = (uint16_t)__float_as_int(idf.y);
@@ -1240,12 +1250,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         tbound = lds_geom;
         tg.geom = lds_geom + nb;
         tg.idx = idx;
-        ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng + p.ncgroups / 2) +
+        ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng + P.ncgroups / 2) +
              (threadIdx.x >> 6);
     }
     if constexpr (kCull == 5) ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom) + (threadIdx.x >> 6);
     if constexpr (kCull == 6) {  // LDS: near/far group boxes, near/far node boxes (whole chunks)
-        const int nb = (p.ncgroups >> 1) * 5, nn = ((p.ncgroups + 63) >> 6) * 20;
+        const int nb = (P.ncgroups >> 1) * 5, nn = ((P.ncgroups + 63) >> 6) * 20;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
         for (int i = threadIdx.x; i < nn; i += blockDim.x) lds_geom[nb + i] = tnode[i];
         __syncthreads();
@@ -1254,13 +1264,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + nn) + (threadIdx.x >> 6);
     }
     const uint32_t lane = threadIdx.x & 63u;
-    const f3 p00 = mk(p.cam[0], p.cam[1], p.cam[2]);
-    const f3 du = mk(p.cam[3], p.cam[4], p.cam[5]);
-    const f3 dv = mk(p.cam[6], p.cam[7], p.cam[8]);
-    const f3 cam = mk(p.cam[9], p.cam[10], p.cam[11]);
-    const uint32_t nchunks = (uint32_t)p.nchunks;
-    const bool reverse = (p.flags & kFlagReverseOrder) != 0;
-    const bool chunk_minor = (p.flags & kFlagChunkMinor) != 0;
+    const f3 p00 = mk(P.cam[0], P.cam[1], P.cam[2]);
+    const f3 du = mk(P.cam[3], P.cam[4], P.cam[5]);
+    const f3 dv = mk(P.cam[6], P.cam[7], P.cam[8]);
+    const f3 cam = mk(P.cam[9], P.cam[10], P.cam[11]);
+    const uint32_t nchunks = (uint32_t)P.nchunks;
+    const bool reverse = (P.flags & kFlagReverseOrder) != 0;
+    const bool chunk_minor = (P.flags & kFlagChunkMinor) != 0;
 
     bool done = false, need = true;
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
@@ -1289,7 +1299,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     unsigned long long t_drained_rt = ~0ull;
 #endif
     // the wave's current block of items (wave-uniform); 64 = exhausted, fetch a new one
-    const uint32_t total_blocks = p.total_items >> 6;
+    const uint32_t total_blocks = P.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
     uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
     bool blk_tail = false;
@@ -1301,9 +1311,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         bool ended = false, fresh_cam = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
         if (best >= 0) {
-            const float4 cr = p.center_radius[best];
-            const float4 sh = p.shade[best];
-            const float4 mat = p.material[best];
+            const float4 cr = P.center_radius[best];
+            const float4 sh = P.shade[best];
+            const float4 mat = P.material[best];
             const f3 point = add(scale(max_t, d), o);
             // normal = (point - centre) / radius: the unscaled division with one reciprocal
             // (exact: candidate_t_fast's argument) for numerators and radius in [2^-40, 2^30]
@@ -1313,7 +1323,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             f3 normal = mk(div_a(pcv.x, cr.w, yr), div_a(pcv.y, cr.w, yr), div_a(pcv.z, cr.w, yr));
             const float nmin = fminf(fminf(fabsf(pcv.x), fabsf(pcv.y)), fabsf(pcv.z));
             const float nmax = fmaxf(fmaxf(fabsf(pcv.x), fabsf(pcv.y)), fabsf(pcv.z));
-            if (!((p.flags & kFlagRadiiSafe) != 0u && nmin >= 0x1p-40f && nmax <= 0x1p30f)) {
+            if (!((P.flags & kFlagRadiiSafe) != 0u && nmin >= 0x1p-40f && nmax <= 0x1p30f)) {
                 asm volatile("");
                 normal = divs(pcv, cr.w);
             }
@@ -1366,7 +1376,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 d = (r1 < reflect_prob) ? reflected : refracted;
             }
             ++pass;
-            if (pass >= p.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
+            if (pass >= P.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
         } else {
             const float len = sqrt_fast(dot(d, d));  // length(d)
             const float t = 0.5f * (d.y / len + 1.0f);
@@ -1379,12 +1389,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             acc = add(acc, contrib);  // the chunk's fp32 sum in sample order
             ++sample;
             if (sample == sample_end) {
-                if ((p.flags & kFlagDirect) != 0u) {
+                if ((P.flags & kFlagDirect) != 0u) {
                     // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
                     const uint32_t out_index =
-                        p.world == 1 ? (pxy >> 16) * (uint32_t)p.width + (pxy & 0xffffu) : q;
-                    p.out[out_index] = make_float4(acc.x / p.spp_total, acc.y / p.spp_total,
-                                                   acc.z / p.spp_total, 1.0f);
+                        P.world == 1 ? (pxy >> 16) * (uint32_t)P.width + (pxy & 0xffffu) : q;
+                    P.out[out_index] = make_float4(acc.x / P.spp_total, acc.y / P.spp_total,
+                                                   acc.z / P.spp_total, 1.0f);
                 } else {
                     // the chunk sum, quantized: RN_even(S * 2^32) (an integer below 2^44),
                     // summed exactly over the pixel's chunks in double; |S| >= 2^12, inf or NaN
@@ -1393,7 +1403,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     const bool ok = amax < kAccumLimit && acc.x == acc.x && acc.y == acc.y &&
                                     acc.z == acc.z;
                     const double nan = __builtin_nan("");
-                    double* s = p.accum + 4u * q;
+                    double* s = P.accum + 4u * q;
 #ifdef VCRT_EXPERIMENT_NO_ATOMICS  // timing experiments only: wrong image
                     if (acc.x == 12345.0f) s[0] = ok ? 1.0 : nan;
 #else
@@ -1404,7 +1414,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 }
                 need = true;
             } else {
-                const float2 jt = p.jitter[sample];
+                const float2 jt = P.jitter[sample];
                 const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
                 o = cam;
                 d = sub(ps, cam);
@@ -1417,6 +1427,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
     };
 
     for (;;) {
+        {  // the argument pointer, opaque to the optimiser (an asm result) and wave-uniform
+           // (readfirstlane: loads through it stay scalar), in the constant address space
+            uint64_t a = reinterpret_cast<uint64_t>(pargs);
+            asm volatile("" : "+s"(a));
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+            pargs = reinterpret_cast<const TraceParams*>(
+                (__attribute__((address_space(4))) const TraceParams*)(((uint64_t)hi << 32) | lo));
+        }
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
         uint64_t t_fetch = 0;
@@ -1431,7 +1450,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 if constexpr (kStats && kCull == 0) ++st_fetch;
                 const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
                 uint32_t b = 0;
-                if ((int)lane == leader) b = atomicAdd(p.work, 1u);
+                if ((int)lane == leader) b = atomicAdd(P.work, 1u);
                 b = __builtin_amdgcn_readfirstlane(__shfl(b, leader));
                 if (b >= total_blocks) {  // queue drained: lanes still wanting work are done
 #ifdef VCRT_WAVE_END_TIMES
@@ -1442,13 +1461,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 }
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
-                blk_tail = b >= p.blocks_head;
-                if (blk_tail) b -= p.blocks_head;
-                if (reverse) b = (blk_tail ? total_blocks - p.blocks_head : p.blocks_head) - 1u - b;
-                blk_nch = blk_tail ? (uint32_t)p.tail_nchunks : nchunks;
+                blk_tail = b >= P.blocks_head;
+                if (blk_tail) b -= P.blocks_head;
+                if (reverse) b = (blk_tail ? total_blocks - P.blocks_head : P.blocks_head) - 1u - b;
+                blk_nch = blk_tail ? (uint32_t)P.tail_nchunks : nchunks;
                 blk_lt = b / blk_nch;
                 blk_chunk = b - blk_lt * blk_nch;
-                tile_of(blk_lt, (uint32_t)p.rank, (uint32_t)p.world, p.tiles_x, &blk_tx, &blk_ty);
+                tile_of(blk_lt, (uint32_t)P.rank, (uint32_t)P.world, P.tiles_x, &blk_tx, &blk_ty);
                 blk_next = 0u;
             }
             const uint32_t avail = 64u - blk_next;
@@ -1462,7 +1481,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 }
                 if (blk_tail) ch |= 0x10000u;  // chunk ch of the tail
                 const uint32_t px = 8u * blk_tx + (slot & 7u), py = 8u * blk_ty + (slot >> 3);
-                if (px < (uint32_t)p.width && py < (uint32_t)p.height) {  // edge tiles: skip
+                if (px < (uint32_t)P.width && py < (uint32_t)P.height) {  // edge tiles: skip
                     got = true;
                     g_lt = blk_lt;
                     g_chunk = ch;
@@ -1481,11 +1500,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             // shader.comp:43  pixel00 + x*delta_u + y*delta_v
             acc = mk(0.f, 0.f, 0.f);
             const bool tail = g_chunk >= 0x10000u;
-            const int k = tail ? p.tail_chunk : p.chunk;
-            sample = (tail ? p.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
-            sample_end = min(sample + k, tail ? p.spp : p.tail_start);
+            const int k = tail ? P.tail_chunk : P.chunk;
+            sample = (tail ? P.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
+            sample_end = min(sample + k, tail ? P.spp : P.tail_start);
             // first camera ray of the chunk, shader.comp:48-52
-            const float2 jt = p.jitter[sample];
+            const float2 jt = P.jitter[sample];
             const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
             o = cam;
             d = sub(ps, cam);
@@ -1512,11 +1531,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
             uint64_t t_cam = 0;
             if constexpr (kStats) t_cam = ticks();
             uint32_t inf = 15u;
-            if (fresh && p.prim_info != nullptr)  // the sphere list of the item's 4x4 quarter
-                inf = p.prim_info[2u * ((q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)) +
+            if (fresh && P.prim_info != nullptr)  // the sphere list of the item's 4x4 quarter
+                inf = P.prim_info[2u * ((q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)) +
                                   1u];
             const float aa = dot(d, d);
-            const bool cam_now = fresh && (inf & 15u) != 15u && (p.flags & kFlagSceneBounded) != 0 &&
+            const bool cam_now = fresh && (inf & 15u) != 15u && (P.flags & kFlagSceneBounded) != 0 &&
                                  aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             float mt = 1e5f;
@@ -1533,16 +1552,16 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     // A camera ray starts at the camera centre: its spheres' oc and cc come from
                     // camera-relative records (pair_disc_cam: same bits, half the arithmetic of
                     // pair_disc_cc); the roots take candidate_t_fast.
-                    cfloat4* crec = (cfloat4*)p.cam_rec;
+                    cfloat4* crec = (cfloat4*)P.cam_rec;
                     const float ya = recip_a(aa);
                     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
-                    for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres (scalar loads)
-                        exact_group_uniform_cam(crec + 4 * gb, (cfloat4*)p.cgroup + 5 * gb, dx, dy,
+                    for (int gb = 0; gb < P.nbig; ++gb)  // the big spheres (scalar loads)
+                        exact_group_uniform_cam(crec + 4 * gb, (cfloat4*)P.cgroup + 5 * gb, dx, dy,
                                                 dz, a2, aa, ya, mt, bst);
                     // the quarter's listed spheres, two per record (primary.cpp): the exact
                     // test's may-hit bits are collected first (bit 2k + s)...
                     const uint32_t cnt = inf & 15u;
-                    const float4* lr = p.cam_rec + 4u * (uint32_t)p.nbig + 3u * (inf >> 4);
+                    const float4* lr = P.cam_rec + 4u * (uint32_t)P.nbig + 3u * (inf >> 4);
                     uint32_t cbits = 0u;
                     for (uint32_t k = 0; 2u * k < cnt; ++k) {
                         ++iters;
@@ -1586,7 +1605,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 }
                 // issued work: the big list and the loop's passes (a pair test is half a group
                 // test), per wave
-                w_groups += (uint64_t)p.nbig;
+                w_groups += (uint64_t)P.nbig;
                 w_pairs += wave_max_small<3>(iters);
             }
             // One shading for the camera rays just traced and the main-scan hits of the last
@@ -1611,7 +1630,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
         if constexpr (kCull != 0) {
             // culling needs every ray of the wave in the guarded finite range (see above)
             const float aa = dot(d, d);
-            const bool guarded = (p.flags & kFlagSceneBounded) != 0 && aa >= 0x1p-20f &&
+            const bool guarded = (P.flags & kFlagSceneBounded) != 0 && aa >= 0x1p-20f &&
                                  aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(!guarded) == 0) {
@@ -1619,14 +1638,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                 uint64_t t0 = 0;
                 if constexpr (kStats) t0 = ticks();
                 if constexpr (kCull == 1)
-                    scan_culled<kStats>(p, o, d, max_t, best, w_groups, w_bounds, hit_groups,
+                    scan_culled<kStats>(P, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kFlat)
                     scan_culled_flat<kStats, kWide, kGRec, kChunks>(
-                        p, tbound, tnode, tg, ws, o, d, pass == 0, q, max_t, best, w_groups,
+                        P, tbound, tnode, tg, ws, o, d, pass == 0, q, max_t, best, w_groups,
                         w_bounds, pt);
                 else
-                    scan_culled_lane<kStats>(p, tbound, tgroup, o, d, max_t, best, w_groups,
+                    scan_culled_lane<kStats>(P, tbound, tgroup, o, d, max_t, best, w_groups,
                                              w_bounds, lane_cnt, hit_groups);
                 if constexpr (kStats) pt.scan += ticks() - t0;
                 if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
@@ -1635,11 +1654,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
                     st_fetch += lane_cnt;
                 }
             } else {
-                scan_spheres<false>(p, lds_geom, n, o, d, max_t, best, hit_groups);
+                scan_spheres<false>(P, lds_geom, n, o, d, max_t, best, hit_groups);
                 w_groups += (uint64_t)((n + 3) >> 2);
             }
         } else {
-            scan_spheres<kLds>(p, lds_geom, n, o, d, max_t, best, hit_groups);
+            scan_spheres<kLds>(P, lds_geom, n, o, d, max_t, best, hit_groups);
             w_groups += (uint64_t)((n + 3) >> 2);
         }
         if constexpr (kStats) st_hitgroups += hit_groups;
@@ -1667,64 +1686,65 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p, float4* lds_dyn
 
 #ifdef VCRT_WAVE_END_TIMES  // diagnostics builds (VCRT_DEBUG_STATS=2): when waves start, end,
                             // and see the queue drained (s_memrealtime, 100 MHz)
-    if (!kStats && lane == 0 && p.debug) {
+    if (!kStats && lane == 0 && P.debug) {
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-        atomicMax(p.debug + 4, t);
-        atomicMin(p.debug + 5, t);
-        atomicAdd(p.debug + 6, t >> 8);
-        atomicAdd(p.debug + 7, 1ull);
-        atomicMin(p.debug + 9, t_start_rt);
-        atomicMin(p.debug + 10, t_drained_rt);
-        atomicAdd(p.debug + 11, t_drained_rt >> 8);
+        atomicMax(P.debug + 4, t);
+        atomicMin(P.debug + 5, t);
+        atomicAdd(P.debug + 6, t >> 8);
+        atomicAdd(P.debug + 7, 1ull);
+        atomicMin(P.debug + 9, t_start_rt);
+        atomicMin(P.debug + 10, t_drained_rt);
+        atomicAdd(P.debug + 11, t_drained_rt >> 8);
     }
 #endif
     // one segment-counter atomic per wave
     unsigned long long total = segs;  // widened before the wave sum
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
-    if (lane == 0 && total) atomicAdd(p.segments, total);
-    if (lane == 0 && p.work_done) {
-        atomicAdd(p.work_done + 0, (unsigned long long)(w_groups + w_pairs / 2u));
-        atomicAdd(p.work_done + 1, (unsigned long long)w_bounds);
+    if (lane == 0 && total) atomicAdd(P.segments, total);
+    if (lane == 0 && P.work_done) {
+        atomicAdd(P.work_done + 0, (unsigned long long)(w_groups + w_pairs / 2u));
+        atomicAdd(P.work_done + 1, (unsigned long long)w_bounds);
     }
     if constexpr (kStats) {
-        if (lane == 0 && p.debug) {
-            atomicAdd(p.debug + 0, (unsigned long long)st_iters);
-            atomicAdd(p.debug + 1, (unsigned long long)st_active);
-            atomicAdd(p.debug + 2, (unsigned long long)st_hitgroups);
-            atomicAdd(p.debug + 3, (unsigned long long)st_fetch);
+        if (lane == 0 && P.debug) {
+            atomicAdd(P.debug + 0, (unsigned long long)st_iters);
+            atomicAdd(P.debug + 1, (unsigned long long)st_active);
+            atomicAdd(P.debug + 2, (unsigned long long)st_hitgroups);
+            atomicAdd(P.debug + 3, (unsigned long long)st_fetch);
             const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-            atomicMax(p.debug + 4, t);
-            atomicMin(p.debug + 5, t);
-            atomicAdd(p.debug + 6, t >> 8);  // mean wave end time (in 256-tick units)
-            atomicAdd(p.debug + 7, 1ull);
-            atomicAdd(p.debug + 8, (unsigned long long)pt.scan);
-            atomicAdd(p.debug + 9, (unsigned long long)pt.levels);
-            atomicAdd(p.debug + 10, (unsigned long long)pt.node);
-            atomicAdd(p.debug + 11, (unsigned long long)pt.group);
-            atomicAdd(p.debug + 12, (unsigned long long)pt.cand);
-            atomicAdd(p.debug + 13, (unsigned long long)pt.cand_passes);
-            atomicAdd(p.debug + 14, (unsigned long long)(ticks() - t_begin));
-            atomicAdd(p.debug + 15, (unsigned long long)pt.big);
-            atomicAdd(p.debug + 16, (unsigned long long)pt.push);
-            atomicAdd(p.debug + 17, (unsigned long long)pt.shade);
-            atomicAdd(p.debug + 18, (unsigned long long)pt.fetch);
-            atomicAdd(p.debug + 19, (unsigned long long)pt.pass_entries);
-            atomicAdd(p.debug + 20, (unsigned long long)pt.pass_lanes);
-            atomicAdd(p.debug + 21, (unsigned long long)pt.partial_passes);
-            atomicAdd(p.debug + 22, (unsigned long long)pt.passes);
-            atomicAdd(p.debug + 23, (unsigned long long)pt.cam);
-            atomicAdd(p.debug + 24, (unsigned long long)pt.cam_entries);
-            atomicAdd(p.debug + 25, (unsigned long long)pt.cam_lanes);
-            atomicAdd(p.debug + 26, (unsigned long long)pt.cam_live);
-            atomicAdd(p.debug + 27, (unsigned long long)pt.list_trips);
-            atomicAdd(p.debug + 28, (unsigned long long)pt.list_sum);
-            atomicAdd(p.debug + 29, (unsigned long long)pt.root_trips);
-            atomicAdd(p.debug + 30, (unsigned long long)pt.root_sum);
-            atomicAdd(p.debug + 31, (unsigned long long)pt.shade_hits);
+            atomicMax(P.debug + 4, t);
+            atomicMin(P.debug + 5, t);
+            atomicAdd(P.debug + 6, t >> 8);  // mean wave end time (in 256-tick units)
+            atomicAdd(P.debug + 7, 1ull);
+            atomicAdd(P.debug + 8, (unsigned long long)pt.scan);
+            atomicAdd(P.debug + 9, (unsigned long long)pt.levels);
+            atomicAdd(P.debug + 10, (unsigned long long)pt.node);
+            atomicAdd(P.debug + 11, (unsigned long long)pt.group);
+            atomicAdd(P.debug + 12, (unsigned long long)pt.cand);
+            atomicAdd(P.debug + 13, (unsigned long long)pt.cand_passes);
+            atomicAdd(P.debug + 14, (unsigned long long)(ticks() - t_begin));
+            atomicAdd(P.debug + 15, (unsigned long long)pt.big);
+            atomicAdd(P.debug + 16, (unsigned long long)pt.push);
+            atomicAdd(P.debug + 17, (unsigned long long)pt.shade);
+            atomicAdd(P.debug + 18, (unsigned long long)pt.fetch);
+            atomicAdd(P.debug + 19, (unsigned long long)pt.pass_entries);
+            atomicAdd(P.debug + 20, (unsigned long long)pt.pass_lanes);
+            atomicAdd(P.debug + 21, (unsigned long long)pt.partial_passes);
+            atomicAdd(P.debug + 22, (unsigned long long)pt.passes);
+            atomicAdd(P.debug + 23, (unsigned long long)pt.cam);
+            atomicAdd(P.debug + 24, (unsigned long long)pt.cam_entries);
+            atomicAdd(P.debug + 25, (unsigned long long)pt.cam_lanes);
+            atomicAdd(P.debug + 26, (unsigned long long)pt.cam_live);
+            atomicAdd(P.debug + 27, (unsigned long long)pt.list_trips);
+            atomicAdd(P.debug + 28, (unsigned long long)pt.list_sum);
+            atomicAdd(P.debug + 29, (unsigned long long)pt.root_trips);
+            atomicAdd(P.debug + 30, (unsigned long long)pt.root_sum);
+            atomicAdd(P.debug + 31, (unsigned long long)pt.shade_hits);
         }
     }
 }
+#undef P
 
 }  // namespace
 
