@@ -534,9 +534,10 @@ KernelChoice select_kernel() {
     // CU, each with its copy); up to the CU's whole LDS with 1024-thread workgroups (one
     // copy for 16 waves); beyond that from global memory.
     const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
-    // flat: near/far boxes (80 B per pair), 64-B group records, uint16 member indices
+    // flat: near/far boxes (80 B per pair, 336 B per node of 4 pairs: 16 B of bank padding),
+    // 64-B group records, uint16 member indices
     const uint32_t tab_lds_flat =
-        static_cast<uint32_t>(16 * (g.ncgroups / 2 * 5 + g.ncgroups * 4) + 8 * g.ncgroups);
+        static_cast<uint32_t>(16 * (g.ncgroups / 8 * 21 + g.ncgroups * 4) + 8 * g.ncgroups);
     const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
     const bool lane_wide = lane_lds && tab_lds > 32768u;
     int variant = g.desc.kernel_variant;
@@ -563,7 +564,7 @@ KernelChoice select_kernel() {
     // Boxes only (near/far group boxes + node boxes of whole chunks) in LDS, one copy for the
     // 16 waves of a 1024-thread workgroup, beside their 16-bit stacks; the records from global.
     const uint32_t box_lds = static_cast<uint32_t>(
-        16 * (g.ncgroups / 2 * 5 + (g.ncgroups + 63) / 64 * 20) + 16 * vcrt::kWaveScratchBytes);
+        16 * (g.ncgroups / 8 * 21 + (g.ncgroups + 63) / 64 * 21) + 16 * vcrt::kWaveScratchBytes);
     // Measured at C5 (stress scene, 4K, 4096 spp, depth 50): 11415 against 11186 Msamples/s
     // with every table in global memory (same bits; profiles/r03_c5_boxes_*).
     const bool flat_boxes = !flat_lds && g.k_trace_cull_flat_boxes != nullptr &&

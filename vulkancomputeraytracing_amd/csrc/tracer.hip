@@ -749,7 +749,7 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 // 1: group, 2: node. Lanes ranked past the entries run on their own ray and push nothing.
 // kKind 0: cand, 1: group, 2: node. n: this stack's height; pushed: the height of the stack
 // this pass pushes onto (group for node passes, cand for group passes).
-template <int kKind, bool kWide, bool kGRec>
+template <int kKind, bool kWide, bool kGRec, uint32_t kNS>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
                                           uint32_t rank, uint32_t lane, WaveScratch<kWide>* ws,
                                           const float4* tbound, const float4* tnode, uint32_t ncg,
@@ -780,7 +780,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         r.c1 = (v2f){c1, c1};
         r.c2 = (v2f){c2, c2};
         // 4 pairs x 80 B: a node's 8 groups, or a chunk's 8 nodes (padded past the last one)
-        const float4* gb = (kKind == 2 ? tbound : tnode) + 20u * (e & F::kMask);
+        const float4* gb = (kKind == 2 ? tbound : tnode) + kNS * (e & F::kMask);
         const NearFarAddr na = near_far_addr(gb, ix, iy, iz);
         uint32_t gout = 0;
 #pragma unroll
@@ -874,7 +874,7 @@ struct FlatStacks {  // wave-uniform stack heights
     uint32_t cand, group, node, chunk;
 };
 
-template <bool kStats, bool kWide, bool kGRec>
+template <bool kStats, bool kWide, bool kGRec, uint32_t kNS>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
                                            WaveScratch<kWide>* ws, FlatStacks& h,
                                            const float4* tbound, const float4* tnode, uint32_t ncg,
@@ -909,22 +909,22 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         else if (nk >= nact) kind = 3;
         else if (th == 1u) kind = nk ? 3 : nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
-            flat_pass<0, kWide, kGRec>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<0, kWide, kGRec, kNS>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (kind == 1) {
             ++n_groups;
-            flat_pass<1, kWide, kGRec>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<1, kWide, kGRec, kNS>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
             n_bounds += 8;
-            flat_pass<2, kWide, kGRec>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<2, kWide, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else if (kind == 3) {
             n_bounds += 8;
-            flat_pass<3, kWide, kGRec>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<3, kWide, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.levels += ticks() - t0;
         } else {
             break;
@@ -939,7 +939,7 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
 // kChunks: the chunk level as per-lane chunk passes over the near/far node boxes `tnode` (many
 // chunks: the stress scene), else wave-uniform node tests on scalar-loaded boxes (two chunks:
 // the final scene).
-template <bool kStats, bool kWide, bool kGRec, bool kChunks>
+template <bool kStats, bool kWide, bool kGRec, bool kChunks, uint32_t kNS>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
                                                  const float4* tnode,
                                                  const GroupTab<kGRec>& tg, WaveScratch<kWide>* ws,
@@ -1056,7 +1056,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             if constexpr (kStats) pt.push += ticks() - t0;
             }
         }
-        flat_drain<kStats, kWide, kGRec>(th, nact, rank, lane, ws, h, tbound, tnode,
+        flat_drain<kStats, kWide, kGRec, kNS>(th, nact, rank, lane, ws, h, tbound, tnode,
                                          (uint32_t)ncg, tg, my, n_groups, n_bounds, pt);
         if (base >= ncg) break;
     }
@@ -1223,6 +1223,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     constexpr bool kWide = kCull == 5;
     constexpr bool kGRec = kCull == 5 || kCull == 6;
     constexpr bool kChunks = kCull == 5 || kCull == 6;
+    // float4s per node record of the near/far box tables (a node's 8 group boxes, a chunk's 8
+    // node boxes: 4 pairs x 80 B): in LDS padded by 16 B, so that the records of nodes n and
+    // n + 2 no longer start on the same LDS bank (stride 84 dwords instead of 80: eight start
+    // banks for the ds_read2_b64 of a 16-lane group instead of two)
+    constexpr uint32_t kNS = (kCull == 4 || kCull == 6) ? 21u : 20u;
     WaveScratch<kWide>* ws = nullptr;
     GroupTab<kGRec> tg{tgroup, nullptr};  // the flat scans' view of the group records
     if constexpr (kCull == 2) {
@@ -1234,8 +1239,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         tgroup = lds_geom + nb;
     }
     if constexpr (kCull == 4) {  // LDS: near/far boxes, 64-B group records, uint16 indices
-        const int nb = (P.ncgroups >> 1) * 5, ng = P.ncgroups * 4;
-        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
+        const int nb = (P.ncgroups >> 3) * kNS, ng = P.ncgroups * 4;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x)
+            if (i % kNS != 20u) lds_geom[i] = tbound[i - i / kNS];
         for (int i = threadIdx.x; i < ng; i += blockDim.x)
             lds_geom[nb + i] = tgroup[5 * (i >> 2) + (i & 3)];
         uint16_t* idx = reinterpret_cast<uint16_t*>(lds_geom + nb + ng);
@@ -1252,12 +1258,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         tg.idx = idx;
         ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng + P.ncgroups / 2) +
              (threadIdx.x >> 6);
+        static_assert(kNS == 21u, "host LDS size (capi.cpp select_kernel)");
     }
     if constexpr (kCull == 5) ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom) + (threadIdx.x >> 6);
     if constexpr (kCull == 6) {  // LDS: near/far group boxes, near/far node boxes (whole chunks)
-        const int nb = (P.ncgroups >> 1) * 5, nn = ((P.ncgroups + 63) >> 6) * 20;
-        for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
-        for (int i = threadIdx.x; i < nn; i += blockDim.x) lds_geom[nb + i] = tnode[i];
+        const int nb = (P.ncgroups >> 3) * kNS, nn = ((P.ncgroups + 63) >> 6) * kNS;
+        for (int i = threadIdx.x; i < nb; i += blockDim.x)
+            if (i % kNS != 20u) lds_geom[i] = tbound[i - i / kNS];
+        for (int i = threadIdx.x; i < nn; i += blockDim.x)
+            if (i % kNS != 20u) lds_geom[nb + i] = tnode[i - i / kNS];
         __syncthreads();
         tbound = lds_geom;
         tnode = lds_geom + nb;
@@ -1641,7 +1650,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     scan_culled<kStats>(P, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kFlat)
-                    scan_culled_flat<kStats, kWide, kGRec, kChunks>(
+                    scan_culled_flat<kStats, kWide, kGRec, kChunks, kNS>(
                         P, tbound, tnode, tg, ws, o, d, pass == 0, q, max_t, best, w_groups,
                         w_bounds, pt);
                 else
