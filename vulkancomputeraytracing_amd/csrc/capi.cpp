@@ -535,9 +535,9 @@ KernelChoice select_kernel() {
     // copy for 16 waves); beyond that from global memory.
     const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
     // flat: near/far boxes (80 B per pair, 336 B per node of 4 pairs: 16 B of bank padding),
-    // 64-B group records, uint16 member indices
+    // 80-B group records (the uint16 member indices inside)
     const uint32_t tab_lds_flat =
-        static_cast<uint32_t>(16 * (g.ncgroups / 8 * 21 + g.ncgroups * 4) + 8 * g.ncgroups);
+        static_cast<uint32_t>(16 * (g.ncgroups / 8 * 21 + g.ncgroups * 5));
     const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
     const bool lane_wide = lane_lds && tab_lds > 32768u;
     int variant = g.desc.kernel_variant;
@@ -587,7 +587,7 @@ KernelChoice select_kernel() {
         f = g.k_trace_cull_flat;
         fs = g.k_trace_cull_flat_stats;
         fname = "vcrt_trace_cull_flat";
-        lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes;
+        lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytesNoChunks;
     } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_boxes) {
         f = g.k_trace_cull_flat_boxes;
         fs = g.k_trace_cull_flat_boxes_stats;

@@ -659,35 +659,35 @@ struct FlatFmt {
     static constexpr uint32_t kMask = (1u << kShift) - 1u;
 };
 
-template <bool kWide>
+template <bool kWide, bool kChunks = true>
 struct WaveScratch {
     using entry_t = typename FlatFmt<kWide>::entry_t;
+    static constexpr bool kHasChunks = kChunks;
     unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
     uint32_t cand[kCandCap];     // group entry << 2 | member
     entry_t group[kGroupCap];    // owner << kShift | group
     entry_t node[kNodeCap];      // owner << kShift | node
-    entry_t chunk[kChunkCap];    // owner << kShift | chunk (64 groups)
+    entry_t chunk[kChunks ? kChunkCap : 0];  // owner << kShift | chunk (64 groups)
 };
 static_assert(sizeof(WaveScratch<false>) == kWaveScratchBytes, "host LDS size");
+static_assert(sizeof(WaveScratch<false, false>) == kWaveScratchBytesNoChunks, "host LDS size");
 static_assert(sizeof(WaveScratch<true>) == kWaveScratchBytesWide, "host LDS size");
 
-// The flat scans' hierarchy group records. Global records (kGRec): the 80-B records of
-// TraceParams.cgroup (four pair-SoA float4s + the members' world[] indices as int bits). LDS
-// records: the four float4s (64 B per group) and the indices as uint16 in a table of their own
-// (8 B per group): 1 KB less LDS per workgroup for the final scene's 128 groups.
+// The flat scans' hierarchy group records, 80 B each: four pair-SoA float4s + the members'
+// world[] indices. Global records (kGRec, TraceParams.cgroup): the indices as int bits. LDS
+// records: the indices as uint16 in the first 8 B of the fifth float4 (the 80-B stride starts
+// 16 consecutive records on 16 different bank quadruples, so the ds_read_b128 of a 16-lane group
+// reading different groups is conflict-free; a 64-B stride gave four).
 template <bool kGRec>
 struct GroupTab {
     const float4* geom;
-    const uint16_t* idx;  // LDS layout only
-    __device__ __forceinline__ const float4* rec(uint32_t gi) const {
-        return geom + (kGRec ? 5u : 4u) * gi;
-    }
+    __device__ __forceinline__ const float4* rec(uint32_t gi) const { return geom + 5u * gi; }
     __device__ __forceinline__ int index(uint32_t gi, uint32_t s) const {
         if constexpr (kGRec) {
             const float4 idf = geom[5u * gi + 4u];
             return __float_as_int(s == 0 ? idf.x : s == 1 ? idf.y : s == 2 ? idf.z : idf.w);
         } else {
-            return (int)idx[4u * gi + s];
+            return (int)reinterpret_cast<const uint16_t*>(geom + 5u * gi + 4u)[s];
         }
     }
 };
@@ -749,9 +749,9 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 // 1: group, 2: node. Lanes ranked past the entries run on their own ray and push nothing.
 // kKind 0: cand, 1: group, 2: node. n: this stack's height; pushed: the height of the stack
 // this pass pushes onto (group for node passes, cand for group passes).
-template <int kKind, bool kWide, bool kGRec, uint32_t kNS>
+template <int kKind, bool kWide, bool kGRec, uint32_t kNS, class WS>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
-                                          uint32_t rank, uint32_t lane, WaveScratch<kWide>* ws,
+                                          uint32_t rank, uint32_t lane, WS* ws,
                                           const float4* tbound, const float4* tnode, uint32_t ncg,
                                           const GroupTab<kGRec>& tg, const FlatRay& my) {
     using F = FlatFmt<kWide>;
@@ -761,9 +761,13 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
     const bool act = rank < m;
     if constexpr (kKind == 2 || kKind == 3) {  // node: the 8 group bounds of (owner, node);
                                                // chunk: the <= 8 node bounds of (owner, chunk)
-        const uint32_t e = act ? (uint32_t)(kKind == 2 ? ws->node[top + rank]
-                                                       : ws->chunk[top + rank])
-                               : (lane << F::kShift);
+        uint32_t e = lane << F::kShift;
+        if (act) {
+            if constexpr (kKind == 2)
+                e = ws->node[top + rank];
+            else
+                e = ws->chunk[top + rank];
+        }
         const int src = (int)(e >> F::kShift) << 2;
         BoxRay r;
         const float ix = from_lane(src, my.br.ix.x), iy = from_lane(src, my.br.iy.x),
@@ -874,9 +878,9 @@ struct FlatStacks {  // wave-uniform stack heights
     uint32_t cand, group, node, chunk;
 };
 
-template <bool kStats, bool kWide, bool kGRec, uint32_t kNS>
+template <bool kStats, bool kWide, bool kGRec, uint32_t kNS, class WS>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
-                                           WaveScratch<kWide>* ws, FlatStacks& h,
+                                           WS* ws, FlatStacks& h,
                                            const float4* tbound, const float4* tnode, uint32_t ncg,
                                            const GroupTab<kGRec>& tg, const FlatRay& my,
                                            uint32_t& n_groups, uint32_t& n_bounds,
@@ -923,9 +927,12 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
             flat_pass<2, kWide, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else if (kind == 3) {
-            n_bounds += 8;
-            flat_pass<3, kWide, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
-            if constexpr (kStats) pt.levels += ticks() - t0;
+            if constexpr (WS::kHasChunks) {  // (nk stays 0 without the chunk stack)
+                n_bounds += 8;
+                flat_pass<3, kWide, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg,
+                                                tg, my);
+                if constexpr (kStats) pt.levels += ticks() - t0;
+            }
         } else {
             break;
         }
@@ -939,10 +946,10 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
 // kChunks: the chunk level as per-lane chunk passes over the near/far node boxes `tnode` (many
 // chunks: the stress scene), else wave-uniform node tests on scalar-loaded boxes (two chunks:
 // the final scene).
-template <bool kStats, bool kWide, bool kGRec, bool kChunks, uint32_t kNS>
+template <bool kStats, bool kWide, bool kGRec, bool kChunks, uint32_t kNS, class WS>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
                                                  const float4* tnode,
-                                                 const GroupTab<kGRec>& tg, WaveScratch<kWide>* ws,
+                                                 const GroupTab<kGRec>& tg, WS* ws,
                                                  const f3 o, const f3 d, bool primary,
                                                  uint32_t item, float& max_t, int& best,
                                                  uint64_t& groups_tested, uint64_t& bounds_tested,
@@ -1228,8 +1235,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     // n + 2 no longer start on the same LDS bank (stride 84 dwords instead of 80: eight start
     // banks for the ds_read2_b64 of a 16-lane group instead of two)
     constexpr uint32_t kNS = (kCull == 4 || kCull == 6) ? 21u : 20u;
-    WaveScratch<kWide>* ws = nullptr;
-    GroupTab<kGRec> tg{tgroup, nullptr};  // the flat scans' view of the group records
+    // the flat scans' per-wave stacks (the LDS-table kernel has no chunk level)
+    using WS = WaveScratch<kWide, kChunks>;
+    WS* ws = nullptr;
+    GroupTab<kGRec> tg{tgroup};  // the flat scans' view of the group records
     if constexpr (kCull == 2) {
         const int nb = (P.ncgroups >> 1) * 4, ng = P.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x) lds_geom[i] = tbound[i];
@@ -1238,29 +1247,29 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         tbound = lds_geom;
         tgroup = lds_geom + nb;
     }
-    if constexpr (kCull == 4) {  // LDS: near/far boxes, 64-B group records, uint16 indices
-        const int nb = (P.ncgroups >> 3) * kNS, ng = P.ncgroups * 4;
+    if constexpr (kCull == 4) {  // LDS: near/far boxes, 80-B group records with uint16 indices
+        const int nb = (P.ncgroups >> 3) * kNS, ng = P.ncgroups * 5;
         for (int i = threadIdx.x; i < nb; i += blockDim.x)
             if (i % kNS != 20u) lds_geom[i] = tbound[i - i / kNS];
-        for (int i = threadIdx.x; i < ng; i += blockDim.x)
-            lds_geom[nb + i] = tgroup[5 * (i >> 2) + (i & 3)];
-        uint16_t* idx = reinterpret_cast<uint16_t*>(lds_geom + nb + ng);
-        for (int i = threadIdx.x; i < P.ncgroups; i += blockDim.x) {
-            const float4 idf = tgroup[5 * i + 4];  // member indices < 2^16 (<= 1024 groups)
-            idx[4 * i + 0] = (uint16_t)__float_as_int(idf.x);
-            idx[4 * i + 1] = (uint16_t)__float_as_int(idf.y);
-            idx[4 * i + 2] = (uint16_t)__float_as_int(idf.z);
-            idx[4 * i + 3] = (uint16_t)__float_as_int(idf.w);
+        for (int i = threadIdx.x; i < ng; i += blockDim.x) {
+            float4 v = tgroup[i];
+            if (i % 5 == 4) {  // member indices < 2^16 (<= 1024 groups), as uint16 (-1: 0xffff)
+                const uint32_t lo = ((uint32_t)__float_as_int(v.x) & 0xffffu) |
+                                    ((uint32_t)__float_as_int(v.y) << 16);
+                const uint32_t hi = ((uint32_t)__float_as_int(v.z) & 0xffffu) |
+                                    ((uint32_t)__float_as_int(v.w) << 16);
+                v = make_float4(__uint_as_float(lo), __uint_as_float(hi), 0.0f, 0.0f);
+            }
+            lds_geom[nb + i] = v;
         }
         __syncthreads();
         tbound = lds_geom;
         tg.geom = lds_geom + nb;
-        tg.idx = idx;
-        ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + ng + P.ncgroups / 2) +
-             (threadIdx.x >> 6);
-        static_assert(kNS == 21u, "host LDS size (capi.cpp select_kernel)");
+        ws = reinterpret_cast<WS*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
+        static_assert(kNS == 21u && sizeof(WS) == kWaveScratchBytesNoChunks,
+                      "host LDS size (capi.cpp select_kernel)");
     }
-    if constexpr (kCull == 5) ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom) + (threadIdx.x >> 6);
+    if constexpr (kCull == 5) ws = reinterpret_cast<WS*>(lds_geom) + (threadIdx.x >> 6);
     if constexpr (kCull == 6) {  // LDS: near/far group boxes, near/far node boxes (whole chunks)
         const int nb = (P.ncgroups >> 3) * kNS, nn = ((P.ncgroups + 63) >> 6) * kNS;
         for (int i = threadIdx.x; i < nb; i += blockDim.x)
@@ -1270,7 +1279,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         __syncthreads();
         tbound = lds_geom;
         tnode = lds_geom + nb;
-        ws = reinterpret_cast<WaveScratch<kWide>*>(lds_geom + nb + nn) + (threadIdx.x >> 6);
+        ws = reinterpret_cast<WS*>(lds_geom + nb + nn) + (threadIdx.x >> 6);
     }
     const uint32_t lane = threadIdx.x & 63u;
     const f3 p00 = mk(P.cam[0], P.cam[1], P.cam[2]);

@@ -85,6 +85,7 @@ struct TraceParams {
 
 constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
 constexpr uint32_t kWaveScratchBytes = 4352;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
+constexpr uint32_t kWaveScratchBytesNoChunks = 4096;  // the same without the chunk stack
 constexpr uint32_t kWaveScratchBytesWide = 6912;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
