@@ -560,7 +560,7 @@ KernelChoice select_kernel() {
     // per 1024-thread workgroup; beyond that the tables stay in global memory and the stacks
     // take 32-bit entries (6.75 KB per wave).
     const bool flat_lds = tab_lds_flat <= 32768u && g.cull_lane_tables != 2 &&
-                          g.cull_lane_tables != 3 && g.ncgroups <= vcrt::kFlatMaxGroups;
+                          g.cull_lane_tables != 3 && g.ncgroups <= vcrt::kFlatMaxGroups8;
     // Boxes only (near/far group boxes + node boxes of whole chunks) in LDS, one copy for the
     // 16 waves of a 1024-thread workgroup, beside their 16-bit stacks; the records from global.
     const uint32_t box_lds = static_cast<uint32_t>(
@@ -587,7 +587,7 @@ KernelChoice select_kernel() {
         f = g.k_trace_cull_flat;
         fs = g.k_trace_cull_flat_stats;
         fname = "vcrt_trace_cull_flat";
-        lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytesNoChunks;
+        lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes8;
     } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_boxes) {
         f = g.k_trace_cull_flat_boxes;
         fs = g.k_trace_cull_flat_boxes_stats;

@@ -649,29 +649,33 @@ constexpr int kNodeCap = 576;
 constexpr int kGroupCap = 576;
 constexpr int kCandCap = 320;
 
-// Stack entries: narrow (16-bit, owner << 10 | index, up to 1024 groups: the LDS-table
-// kernel) or wide (32-bit, owner << 24 | index: the global-table kernel for large scenes).
-// Candidate entries are 32-bit either way: (node/group entry) << 2 | member.
-template <bool kWide>
+// Stack entries, by format kFmt:
+//   0 (narrow8, the LDS-table kernel, <= 256 groups): 16-bit owner << 8 | index, and 16-bit
+//     candidate entries (node/group entry) << 2 | member;
+//   1 (narrow10, the boxes-in-LDS kernel, <= 1024 groups): 16-bit owner << 10 | index,
+//     32-bit candidate entries;
+//   2 (wide, the global-table kernel, any size): 32-bit owner << 24 | index and candidates.
+template <int kFmt>
 struct FlatFmt {
-    using entry_t = typename std::conditional<kWide, uint32_t, uint16_t>::type;
-    static constexpr int kShift = kWide ? 24 : 10;  // owner field of node / group entries
+    using entry_t = typename std::conditional<kFmt == 2, uint32_t, uint16_t>::type;
+    using cand_t = typename std::conditional<kFmt == 0, uint16_t, uint32_t>::type;
+    static constexpr int kShift = kFmt == 2 ? 24 : kFmt == 1 ? 10 : 8;  // owner field
     static constexpr uint32_t kMask = (1u << kShift) - 1u;
 };
 
-template <bool kWide, bool kChunks = true>
+template <int kFmt, bool kChunks = true>
 struct WaveScratch {
-    using entry_t = typename FlatFmt<kWide>::entry_t;
+    using entry_t = typename FlatFmt<kFmt>::entry_t;
     static constexpr bool kHasChunks = kChunks;
     unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
-    uint32_t cand[kCandCap];     // group entry << 2 | member
+    typename FlatFmt<kFmt>::cand_t cand[kCandCap];  // group entry << 2 | member
     entry_t group[kGroupCap];    // owner << kShift | group
     entry_t node[kNodeCap];      // owner << kShift | node
     entry_t chunk[kChunks ? kChunkCap : 0];  // owner << kShift | chunk (64 groups)
 };
-static_assert(sizeof(WaveScratch<false>) == kWaveScratchBytes, "host LDS size");
-static_assert(sizeof(WaveScratch<false, false>) == kWaveScratchBytesNoChunks, "host LDS size");
-static_assert(sizeof(WaveScratch<true>) == kWaveScratchBytesWide, "host LDS size");
+static_assert(sizeof(WaveScratch<0>) == kWaveScratchBytes8, "host LDS size");
+static_assert(sizeof(WaveScratch<1>) == kWaveScratchBytes, "host LDS size");
+static_assert(sizeof(WaveScratch<2>) == kWaveScratchBytesWide, "host LDS size");
 
 // The flat scans' hierarchy group records, 80 B each: four pair-SoA float4s + the members'
 // world[] indices. Global records (kGRec, TraceParams.cgroup): the indices as int bits. LDS
@@ -749,12 +753,12 @@ struct FlatRay {  // this lane's ray, as the passes fetch it
 // 1: group, 2: node. Lanes ranked past the entries run on their own ray and push nothing.
 // kKind 0: cand, 1: group, 2: node. n: this stack's height; pushed: the height of the stack
 // this pass pushes onto (group for node passes, cand for group passes).
-template <int kKind, bool kWide, bool kGRec, uint32_t kNS, class WS>
+template <int kKind, int kFmt, bool kGRec, uint32_t kNS, class WS>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
                                           uint32_t rank, uint32_t lane, WS* ws,
                                           const float4* tbound, const float4* tnode, uint32_t ncg,
                                           const GroupTab<kGRec>& tg, const FlatRay& my) {
-    using F = FlatFmt<kWide>;
+    using F = FlatFmt<kFmt>;
     using entry_t = typename F::entry_t;
     const uint32_t m = min(n, nact), top = n - m;
     n = top;
@@ -833,7 +837,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
             do {
                 const uint32_t s = (uint32_t)__builtin_ctz(hits);
                 hits &= hits - 1;
-                ws->cand[pos++] = tag | s;
+                ws->cand[pos++] = (typename F::cand_t)(tag | s);
             } while (hits);
         }
     } else {  // cand: the member's root (its hb, cc, disc recomputed as the packed test did)
@@ -878,7 +882,7 @@ struct FlatStacks {  // wave-uniform stack heights
     uint32_t cand, group, node, chunk;
 };
 
-template <bool kStats, bool kWide, bool kGRec, uint32_t kNS, class WS>
+template <bool kStats, int kFmt, bool kGRec, uint32_t kNS, class WS>
 __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t rank, uint32_t lane,
                                            WS* ws, FlatStacks& h,
                                            const float4* tbound, const float4* tnode, uint32_t ncg,
@@ -913,23 +917,23 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         else if (nk >= nact) kind = 3;
         else if (th == 1u) kind = nk ? 3 : nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
-            flat_pass<0, kWide, kGRec, kNS>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<0, kFmt, kGRec, kNS>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (kind == 1) {
             ++n_groups;
-            flat_pass<1, kWide, kGRec, kNS>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<1, kFmt, kGRec, kNS>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
             n_bounds += 8;
-            flat_pass<2, kWide, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<2, kFmt, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else if (kind == 3) {
             if constexpr (WS::kHasChunks) {  // (nk stays 0 without the chunk stack)
                 n_bounds += 8;
-                flat_pass<3, kWide, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg,
+                flat_pass<3, kFmt, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg,
                                                 tg, my);
                 if constexpr (kStats) pt.levels += ticks() - t0;
             }
@@ -946,7 +950,7 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
 // kChunks: the chunk level as per-lane chunk passes over the near/far node boxes `tnode` (many
 // chunks: the stress scene), else wave-uniform node tests on scalar-loaded boxes (two chunks:
 // the final scene).
-template <bool kStats, bool kWide, bool kGRec, bool kChunks, uint32_t kNS, class WS>
+template <bool kStats, int kFmt, bool kGRec, bool kChunks, uint32_t kNS, class WS>
 __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const float4* tbound,
                                                  const float4* tnode,
                                                  const GroupTab<kGRec>& tg, WS* ws,
@@ -1001,7 +1005,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
         const uint16_t* ids = p.prim_ids + loff;
         for (uint32_t k = 0; k < lcnt; ++k)
             ws->group[pos++] =
-                (typename FlatFmt<kWide>::entry_t)((lane << FlatFmt<kWide>::kShift) | ids[k]);
+                (typename FlatFmt<kFmt>::entry_t)((lane << FlatFmt<kFmt>::kShift) | ids[k]);
     }
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* top = (cfloat4*)p.ctop;
@@ -1026,8 +1030,8 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             // level 1 (many chunks): a chunk entry per lane whose ray may meet the chunk; chunk
             // passes test its nodes for that lane alone
             if (in_chunk)
-                ws->chunk[h.chunk + lanes_below(want)] = (typename FlatFmt<kWide>::entry_t)(
-                    (lane << FlatFmt<kWide>::kShift) | ((uint32_t)base >> 6));
+                ws->chunk[h.chunk + lanes_below(want)] = (typename FlatFmt<kFmt>::entry_t)(
+                    (lane << FlatFmt<kFmt>::kShift) | ((uint32_t)base >> 6));
             h.chunk += (uint32_t)__popcll(want);
             if constexpr (kStats) pt.push += ticks() - t0;
             } else {
@@ -1053,17 +1057,17 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             uint32_t pos = h.node + wave_prefix<4>((uint32_t)__popc(nodes), tot);
             h.node += tot;
             if (nodes) {
-                const uint32_t tag = (lane << FlatFmt<kWide>::kShift) | ((uint32_t)base >> 3);
+                const uint32_t tag = (lane << FlatFmt<kFmt>::kShift) | ((uint32_t)base >> 3);
                 do {
                     const uint32_t j = (uint32_t)__builtin_ctz(nodes);
                     nodes &= nodes - 1;
-                    ws->node[pos++] = (typename FlatFmt<kWide>::entry_t)(tag | j);
+                    ws->node[pos++] = (typename FlatFmt<kFmt>::entry_t)(tag | j);
                 } while (nodes);
             }
             if constexpr (kStats) pt.push += ticks() - t0;
             }
         }
-        flat_drain<kStats, kWide, kGRec, kNS>(th, nact, rank, lane, ws, h, tbound, tnode,
+        flat_drain<kStats, kFmt, kGRec, kNS>(th, nact, rank, lane, ws, h, tbound, tnode,
                                          (uint32_t)ncg, tg, my, n_groups, n_bounds, pt);
         if (base >= ncg) break;
     }
@@ -1227,16 +1231,20 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     // the flat scan's stacks: after the LDS tables (kCull 4: all tables; kCull 6: the boxes,
     // with the group records in global memory), or alone with the tables in global memory and
     // 32-bit entries (kCull 5)
-    constexpr bool kWide = kCull == 5;
+    constexpr int kFmt = kCull == 5 ? 2 : kCull == 6 ? 1 : 0;  // stack entry format
     constexpr bool kGRec = kCull == 5 || kCull == 6;
+#ifdef VCRT_AB_LDS_CHUNK_PASSES  // A/B builds: the LDS-table kernel with per-lane chunk passes
+    constexpr bool kChunks = kCull == 4 || kCull == 5 || kCull == 6;
+#else
     constexpr bool kChunks = kCull == 5 || kCull == 6;
+#endif
     // float4s per node record of the near/far box tables (a node's 8 group boxes, a chunk's 8
     // node boxes: 4 pairs x 80 B): in LDS padded by 16 B, so that the records of nodes n and
     // n + 2 no longer start on the same LDS bank (stride 84 dwords instead of 80: eight start
     // banks for the ds_read2_b64 of a 16-lane group instead of two)
     constexpr uint32_t kNS = (kCull == 4 || kCull == 6) ? 21u : 20u;
     // the flat scans' per-wave stacks (the LDS-table kernel has no chunk level)
-    using WS = WaveScratch<kWide, kChunks>;
+    using WS = WaveScratch<kFmt, kChunks>;
     WS* ws = nullptr;
     GroupTab<kGRec> tg{tgroup};  // the flat scans' view of the group records
     if constexpr (kCull == 2) {
@@ -1266,7 +1274,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         tbound = lds_geom;
         tg.geom = lds_geom + nb;
         ws = reinterpret_cast<WS*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
-        static_assert(kNS == 21u && sizeof(WS) == kWaveScratchBytesNoChunks,
+        static_assert(kNS == 21u && sizeof(WS) <= kWaveScratchBytes8,
                       "host LDS size (capi.cpp select_kernel)");
     }
     if constexpr (kCull == 5) ws = reinterpret_cast<WS*>(lds_geom) + (threadIdx.x >> 6);
@@ -1659,7 +1667,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     scan_culled<kStats>(P, o, d, max_t, best, w_groups, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kFlat)
-                    scan_culled_flat<kStats, kWide, kGRec, kChunks, kNS>(
+                    scan_culled_flat<kStats, kFmt, kGRec, kChunks, kNS>(
                         P, tbound, tnode, tg, ws, o, d, pass == 0, q, max_t, best, w_groups,
                         w_bounds, pt);
                 else

@@ -83,9 +83,10 @@ struct TraceParams {
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
 };
 
-constexpr int32_t kFlatMaxGroups = 1024;       // CULL_FLAT: 10-bit group / node fields
-constexpr uint32_t kWaveScratchBytes = 4352;      // CULL_FLAT per-wave LDS stacks, 16-bit entries
-constexpr uint32_t kWaveScratchBytesNoChunks = 4096;  // the same without the chunk stack
+constexpr int32_t kFlatMaxGroups = 1024;   // CULL_FLAT 16-bit entries: 10-bit group / node fields
+constexpr int32_t kFlatMaxGroups8 = 256;   // the LDS-table kernel: 8-bit fields, 16-bit candidates
+constexpr uint32_t kWaveScratchBytes = 4352;   // CULL_FLAT per-wave LDS stacks, 16-bit entries
+constexpr uint32_t kWaveScratchBytes8 = 3712;  // the same with 16-bit candidate entries
 constexpr uint32_t kWaveScratchBytesWide = 6912;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
