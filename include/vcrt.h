@@ -130,7 +130,7 @@ typedef struct vcrt_stats {
     int32_t grid_blocks, block_threads, kernel_variant;
     int32_t local_tiles;   /* 8x8 tiles this rank renders */
     int32_t nspheres;
-    uint32_t lds_bytes;
+    uint32_t lds_bytes;    /* dynamic LDS of the tracer's tables and stacks (without the ring) */
     int32_t accumulate_chunk; /* samples per work item in effect */
     int32_t tables_in_lds;    /* 1 when the culled scan reads its tables from LDS, 2 when only
                                  its boxes (vcrt_trace_cull_flat_boxes) */
@@ -150,6 +150,9 @@ typedef struct vcrt_stats {
                            lane sum, root loop trips and lane sum; main-scan hit lanes */
     int32_t accumulate_tail;       /* tail samples per pixel in effect (0: none) */
     int32_t accumulate_tail_chunk; /* samples per tail item in effect */
+    int32_t ring_entries;          /* LDS accumulation ring entries per wave (0: none; the chunk
+                                      sums go to global memory directly) */
+    int32_t reserved0;
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

@@ -693,3 +693,33 @@ def test_stats_name_the_launched_kernel(scene, variant, kernel):
     object symbol the frame dispatched: what bench.py reports and rocprof lists."""
     _, st = gpu_render(scene, 64, 36, 1, 4, variant)
     assert st["kernel"] == kernel
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,tail,tail_chunk,ring", [
+    ("final", 64, 36, 40, 10, 8, 12, 5, "0"),       # ring off: chunk sums straight to memory
+    ("final", 64, 36, 40, 10, 8, 12, 5, "8"),       # a small ring: entries recycled often
+    ("three", 37, 23, 48, 8, 4, 0, 0, "1"),         # ragged edge tiles, 12 chunks per pixel
+    ("final", 50, 30, 33, 10, 7, 0, 0, "1"),        # 5 chunks: blocks straddle pixels
+    ("stress4096", 40, 24, 20, 12, 4, 8, 2, "1"),  # the boxes-in-LDS kernel's ring
+])
+def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth, chunk, tail,
+                                   tail_chunk, ring):
+    """The per-wave LDS accumulation ring (tracer.hip RingEntry): chunk sums added in LDS and
+    flushed per pixel give the same exact sums as adding every chunk sum to global memory."""
+    monkeypatch.setenv("VCRT_ACCUM_RING", ring)
+    k = chunk_of(w, h, spp, chunk, tail=tail, tail_chunk=tail_chunk)
+    want, want_segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         accumulate_chunk=chunk, accumulate_tail=tail,
+                         accumulate_tail_chunk=tail_chunk)
+    with vc.Renderer(desc, scene) as r:
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    assert_bitwise(got, want, f"{scene} ring={ring}")
+    assert st["segments"] == want_segs
+    if ring == "0":
+        assert st["ring_entries"] == 0
+    elif ring == "8":
+        assert st["ring_entries"] == 8
+    else:
+        assert st["ring_entries"] >= 8

@@ -28,4 +28,12 @@ if [ -n "$STRESS" ]; then
   run "new stress" python tools/ab.py default --rounds 1 $S
   for o in $OBJS; do run "$o stress" python tools/ab.py $o --rounds 1 $S; done
 fi
+if [ -n "$C2" ]; then
+  C2A="--scene three --width 800 --height 450 --spp 64 --depth 8 --frames 20"
+  for i in 1 2 3; do
+    run "prev c2" env VCRT_PKG_ROOT=ab_objs/prev python tools/ab.py default --rounds 1 $C2A
+    run "new c2" python tools/ab.py default --rounds 1 $C2A
+    for o in $OBJS; do run "$o c2" python tools/ab.py $o --rounds 1 $C2A; done
+  done
+fi
 echo ab_done

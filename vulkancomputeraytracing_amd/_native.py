@@ -106,6 +106,8 @@ class vcrt_stats(ctypes.Structure):
         ("debug", ctypes.c_uint64 * 32),
         ("accumulate_tail", ctypes.c_int32),
         ("accumulate_tail_chunk", ctypes.c_int32),
+        ("ring_entries", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
     ]
 
 

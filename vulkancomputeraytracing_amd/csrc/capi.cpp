@@ -58,6 +58,9 @@ struct RendererState {
                   k_trace_cull_flat_boxes_stats = nullptr;
     // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global, 3 = boxes in LDS (flat scan)
     int cull_lane_tables = 0;
+    bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
+    uint32_t ring_max = vcrt::kRingMaxEntries;
+    uint32_t lds_per_cu = 0;     // LDS bytes per CU (160 KB on gfx950)
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     int debug_stats = 0;  // 1: the stats kernels; 2: the product kernels with a debug buffer
                           //    (builds with VCRT_WAVE_END_TIMES record wave start/end times)
@@ -683,6 +686,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         return fail(VCRT_ERROR_FEATURE_NOT_PRESENT);  // code object is gfx950-only
     g.num_cus = prop.multiProcessorCount;
     g.max_lds = prop.sharedMemPerBlock;
+    g.lds_per_cu = static_cast<uint32_t>(prop.maxSharedMemoryPerMultiProcessor);
     if ((r = to_vk(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking))) != VK_SUCCESS)
         return fail(r);
     if ((r = to_vk(hipEventCreate(&g.ev_start))) != VK_SUCCESS) return fail(r);
@@ -782,6 +786,10 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     g.work_flags |= vcrt::kFlagChunkMinor;
     if (const char* e = std::getenv("VCRT_ITEM_ORDER"))
         if (std::strcmp(e, "tile") == 0) g.work_flags &= ~vcrt::kFlagChunkMinor;
+    if (const char* e = std::getenv("VCRT_ACCUM_RING")) {  // 0: off; n > 1: at most n entries
+        g.accum_ring = std::atoi(e) != 0;
+        if (std::atoi(e) > 1) g.ring_max = static_cast<uint32_t>(std::atoi(e));
+    }
     if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, sizeof(g.stats.debug)))) != VK_SUCCESS)
         return fail(r);
 
@@ -1031,6 +1039,40 @@ vcrt_result vcrt_draw_next_frame(void) {
                 per_cu <= 0)
                 per_cu = 1;
         }
+        // The accumulation ring (tracer.hip RingEntry): the LDS the workgroups leave free at
+        // this occupancy, up to 63 entries of 32 B per wave, when the frame sums chunk sums
+        // (not one chunk per pixel), its blocks are chunk-minor and its pixel indices leave the
+        // top bits for the entry. The occupancy must not drop for it.
+        p.ring_off = 0u;
+        p.ring_n = 0u;
+        uint32_t lds_launch = lds;
+        if (g.accum_ring && !g.direct && (g.work_flags & vcrt::kFlagChunkMinor) != 0u &&
+            static_cast<uint64_t>(g.local_tiles) * 64u <= (uint64_t{1} << vcrt::kRingQBits) &&
+            g.lds_per_cu > 0 && g.desc.blocks_per_cu <= 0) {
+            const uint32_t waves = block / 64u;
+            const uint32_t off = (lds + 15u) & ~15u;
+            // usable LDS per CU: measured, five 256-thread workgroups of 32512 B ran four per
+            // CU (-11% at C4) while 32000 B ran five, although 5 x 32512 < 160 KiB and the
+            // occupancy query allows them: budget 160000 B per CU
+            const uint32_t per_wg = std::min<uint32_t>(g.lds_per_cu, 160000u) /
+                                    static_cast<uint32_t>(per_cu);
+            uint32_t n = per_wg > off ? std::min<uint32_t>(g.ring_max,
+                                                            (per_wg - off) / (32u * waves))
+                                      : 0u;
+            for (; n >= 8u; n -= 4u) {
+                int occ = 0;
+                if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(
+                        &occ, f, block, off + 32u * n * waves) == hipSuccess &&
+                    occ >= per_cu)
+                    break;
+            }
+            if (n >= 8u) {
+                p.ring_off = off;
+                p.ring_n = n;
+                lds_launch = off + 32u * n * waves;
+            }
+        }
+        g.stats.ring_entries = static_cast<int32_t>(p.ring_n);
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
         VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
         if (!g.direct && !g.desc.progressive)  // every frame sums from zero
@@ -1042,7 +1084,7 @@ vcrt_result vcrt_draw_next_frame(void) {
                                     g.stream));
         }
         VCRT_TRY(hipEventRecord(g.ev_start, g.stream));
-        VkResult r = launch(f, grid, block, lds, p);
+        VkResult r = launch(f, grid, block, lds_launch, p);
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
         if (!g.direct) {
@@ -1074,7 +1116,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         g.stats.grid_blocks = static_cast<int32_t>(grid);
         g.stats.block_threads = static_cast<int32_t>(block);
         g.stats.kernel_variant = variant;
-        g.stats.lds_bytes = lds;
+        g.stats.lds_bytes = lds;  // tables and stacks; the ring adds ring_entries x 32 B per wave
         g.stats.tables_in_lds = kc.f == g.k_trace_cull_flat_boxes ? 2 :
                                 (kc.f == g.k_trace_cull_flat || kc.f == g.k_trace_cull_lane_lds ||
                                  kc.f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;

@@ -673,7 +673,7 @@ struct WaveScratch {
     entry_t node[kNodeCap];      // owner << kShift | node
     entry_t chunk[kChunks ? kChunkCap : 0];  // owner << kShift | chunk (64 groups)
 };
-static_assert(sizeof(WaveScratch<0>) == kWaveScratchBytes8, "host LDS size");
+static_assert(sizeof(WaveScratch<0, false>) == kWaveScratchBytes8, "host LDS size");
 static_assert(sizeof(WaveScratch<1>) == kWaveScratchBytes, "host LDS size");
 static_assert(sizeof(WaveScratch<2>) == kWaveScratchBytesWide, "host LDS size");
 
@@ -1182,6 +1182,51 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
     groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
 }
 
+// ---- Accumulation ring ---------------------------------------------------------------------
+// Each wave keeps the chunk sums of its current blocks' pixels in LDS: a ring of 32-B entries
+// (pixel, three double sums). A block (64 items: all chunks of a few pixels in chunk-minor order)
+// takes the next entries of the ring for its pixels, flushing what they held -- partial sums of
+// an older block's pixels -- to the pixels' global sums with one f64 atomic per channel; a
+// finished item adds its quantized chunk sums to its pixel's entry with LDS atomics (ds_add_f64)
+// if the entry still holds that pixel, else straight to the global sums as before. The sums are
+// integers below 2^53 (vcrt_math.h "Accumulation"), so every partition of the additions gives
+// the same exact total: the image bits do not depend on which additions went through LDS.
+// NaN chunk sums add NaN either way. Each wave flushes its ring before it ends.
+struct RingEntry {
+    uint32_t q;  // local pixel index, ~0: none
+    uint32_t pad;
+    double s[3];
+};
+static_assert(sizeof(RingEntry) == 32, "host LDS size");
+constexpr uint32_t kQMask = (1u << kRingQBits) - 1u;  // a lane's pixel index without the entry
+
+__device__ __forceinline__ void ring_flush(RingEntry& e, double* accum) {
+    if (e.q != ~0u) {
+        double* g = accum + 4u * e.q;
+        // exact zeros add nothing (+0 + -0 = +0: the sums start at +0); one channel at a time
+        // (few registers: this runs in the block fetch, where the whole lane state is live)
+#pragma unroll 1
+        for (int c = 0; c < 3; ++c) {
+            const double v = e.s[c];
+            if (v != 0.0) atomicAdd(g + c, v);
+        }
+    }
+}
+
+// A ring block's entry for pixel slot `slot` of local tile lt at tile (txy & 0xffff, txy >> 16):
+// flushes the entry's old sums, then holds that pixel with zero sums.
+__device__ __forceinline__ void ring_claim(RingEntry* ring, uint32_t ei, uint32_t rn,
+                                                     double* accum, uint32_t slot, uint32_t lt,
+                                                     uint32_t txy, uint32_t width,
+                                                     uint32_t height) {
+    if (ei >= rn) ei -= rn;
+    RingEntry& re = ring[ei];
+    ring_flush(re, accum);
+    const uint32_t px = 8u * (txy & 0xffffu) + (slot & 7u), py = 8u * (txy >> 16) + (slot >> 3);
+    re.q = (slot < 64u && px < width && py < height) ? lt * 64u + slot : ~0u;
+    re.s[0] = re.s[1] = re.s[2] = 0.0;
+}
+
 // Local element q = 64 * lt + slot of this rank -> pixel (x, y) and its framebuffer index.
 struct Pixel {
     uint32_t x, y, out_index;
@@ -1233,11 +1278,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     // 32-bit entries (kCull 5)
     constexpr int kFmt = kCull == 5 ? 2 : kCull == 6 ? 1 : 0;  // stack entry format
     constexpr bool kGRec = kCull == 5 || kCull == 6;
-#ifdef VCRT_AB_LDS_CHUNK_PASSES  // A/B builds: the LDS-table kernel with per-lane chunk passes
-    constexpr bool kChunks = kCull == 4 || kCull == 5 || kCull == 6;
-#else
     constexpr bool kChunks = kCull == 5 || kCull == 6;
-#endif
     // float4s per node record of the near/far box tables (a node's 8 group boxes, a chunk's 8
     // node boxes: 4 pairs x 80 B): in LDS padded by 16 B, so that the records of nodes n and
     // n + 2 no longer start on the same LDS bank (stride 84 dwords instead of 80: eight start
@@ -1274,7 +1315,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         tbound = lds_geom;
         tg.geom = lds_geom + nb;
         ws = reinterpret_cast<WS*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
-        static_assert(kNS == 21u && sizeof(WS) <= kWaveScratchBytes8,
+        static_assert(kNS == 21u && sizeof(WS) == kWaveScratchBytes8,
                       "host LDS size (capi.cpp select_kernel)");
     }
     if constexpr (kCull == 5) ws = reinterpret_cast<WS*>(lds_geom) + (threadIdx.x >> 6);
@@ -1299,6 +1340,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     const bool chunk_minor = (P.flags & kFlagChunkMinor) != 0;
 
     bool done = false, need = true;
+    bool fin = false;  // the lane's chunk is finished and its sum in acc not yet added
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
     // flat scan: a main-scan hit waits for the next iteration's shading (pend_t, pend_best;
     // pend_best < 0: none), which it shares with that iteration's camera rays
@@ -1329,6 +1371,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
     uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
     bool blk_tail = false;
+    // the wave's accumulation ring (see RingEntry): next entry to hand out; the current block's
+    // first pixel slot and first entry + 1 (0: the block's items add to global memory)
+    RingEntry* const ring =
+        P.ring_n ? reinterpret_cast<RingEntry*>(reinterpret_cast<char*>(lds_dyn) + P.ring_off) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * P.ring_n
+                 : nullptr;
+    uint32_t ring_pos = 0u, blk_ps0 = 0u, blk_ring = 0u;
+    if (ring) {
+        for (uint32_t i = lane; i < P.ring_n; i += 64u) ring[i].q = ~0u;
+        __builtin_amdgcn_wave_barrier();
+    }
 
     // Shades a traced segment (textures.glsl, or the sky of functions.glsl:85-89) and advances
     // the lane's path: accumulate and start the next sample's camera ray (returns true), or
@@ -1415,29 +1468,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             acc = add(acc, contrib);  // the chunk's fp32 sum in sample order
             ++sample;
             if (sample == sample_end) {
-                if ((P.flags & kFlagDirect) != 0u) {
-                    // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
-                    const uint32_t out_index =
-                        P.world == 1 ? (pxy >> 16) * (uint32_t)P.width + (pxy & 0xffffu) : q;
-                    P.out[out_index] = make_float4(acc.x / P.spp_total, acc.y / P.spp_total,
-                                                   acc.z / P.spp_total, 1.0f);
-                } else {
-                    // the chunk sum, quantized: RN_even(S * 2^32) (an integer below 2^44),
-                    // summed exactly over the pixel's chunks in double; |S| >= 2^12, inf or NaN
-                    // make the pixel NaN (vcrt_math.h "Accumulation")
-                    const float amax = fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fabsf(acc.z));
-                    const bool ok = amax < kAccumLimit && acc.x == acc.x && acc.y == acc.y &&
-                                    acc.z == acc.z;
-                    const double nan = __builtin_nan("");
-                    double* s = P.accum + 4u * q;
-#ifdef VCRT_EXPERIMENT_NO_ATOMICS  // timing experiments only: wrong image
-                    if (acc.x == 12345.0f) s[0] = ok ? 1.0 : nan;
-#else
-                    atomicAdd(s + 0, ok ? (double)__builtin_rintf(acc.x * kAccumScale) : nan);
-                    atomicAdd(s + 1, ok ? (double)__builtin_rintf(acc.y * kAccumScale) : nan);
-                    atomicAdd(s + 2, ok ? (double)__builtin_rintf(acc.z * kAccumScale) : nan);
-#endif
-                }
+                // the chunk is done: its sum in acc is retired at the top of the next iteration
+                // (few registers are live there: the accumulation code stays out of shading)
+                fin = true;
                 need = true;
             } else {
                 const float2 jt = P.jitter[sample];
@@ -1462,6 +1495,46 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             pargs = reinterpret_cast<const TraceParams*>(
                 (__attribute__((address_space(4))) const TraceParams*)(((uint64_t)hi << 32) | lo));
         }
+        if (fin) {  // ---- retire the finished chunk: its sum to the pixel ----
+            fin = false;
+            if ((P.flags & kFlagDirect) != 0u) {
+                // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
+                const uint32_t out_index =
+                    P.world == 1 ? (pxy >> 16) * (uint32_t)P.width + (pxy & 0xffffu) : q & kQMask;
+                P.out[out_index] = make_float4(acc.x / P.spp_total, acc.y / P.spp_total,
+                                               acc.z / P.spp_total, 1.0f);
+            } else {
+                // the chunk sum, quantized: RN_even(S * 2^32) (an integer below 2^44), summed
+                // exactly over the pixel's chunks in double; |S| >= 2^12, inf or NaN make the
+                // pixel NaN (vcrt_math.h "Accumulation")
+                const float amax = fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fabsf(acc.z));
+                const bool ok = amax < kAccumLimit && acc.x == acc.x && acc.y == acc.y &&
+                                acc.z == acc.z;
+                const double nan = __builtin_nan("");
+                const double v0 = ok ? (double)__builtin_rintf(acc.x * kAccumScale) : nan;
+                const double v1 = ok ? (double)__builtin_rintf(acc.y * kAccumScale) : nan;
+                const double v2 = ok ? (double)__builtin_rintf(acc.z * kAccumScale) : nan;
+                const uint32_t qi = q & kQMask, ent = q >> kRingQBits;
+                // the pixel's ring entry while it still holds this pixel (LDS atomics), else
+                // global memory (two branches: a pointer that may be either would make flat
+                // atomics, whose completion every later LDS wait would wait for)
+                if (ent != 0u && ring[ent - 1u].q == qi) {
+                    double* s = ring[ent - 1u].s;
+                    atomicAdd(s + 0, v0);
+                    atomicAdd(s + 1, v1);
+                    atomicAdd(s + 2, v2);
+                } else {
+                    double* s = P.accum + 4u * qi;
+#ifdef VCRT_EXPERIMENT_NO_ATOMICS  // timing experiments only: wrong image
+                    if (acc.x == 12345.0f) s[0] = v0;
+#else
+                    atomicAdd(s + 0, v0);
+                    atomicAdd(s + 1, v1);
+                    atomicAdd(s + 2, v2);
+#endif
+                }
+            }
+        }
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
         uint64_t t_fetch = 0;
@@ -1469,7 +1542,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         // The loop only hands out slots; the lane state is set up once after it (setting it up
         // inside made the compiler copy ~20 live registers around the loop on every pass).
         bool got = false;
-        uint32_t g_lt = 0u, g_chunk = 0u, g_slot = 0u, g_px = 0u, g_py = 0u;
+        uint32_t g_lt = 0u, g_chunk = 0u, g_slot = 0u, g_px = 0u, g_py = 0u, g_ent = 0u;
         uint64_t need_mask = __ballot(need && !done);
         while (need_mask) {
             if (blk_next >= 64u) {
@@ -1495,6 +1568,25 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 blk_chunk = b - blk_lt * blk_nch;
                 tile_of(blk_lt, (uint32_t)P.rank, (uint32_t)P.world, P.tiles_x, &blk_tx, &blk_ty);
                 blk_next = 0u;
+                // ring entries for the block's pixel slots ps0 .. ps1 (chunk-minor items
+                // 64 c .. 64 c + 63 of the tile are (i / nch, i % nch)): flushed and set up by
+                // one lane each (the loop top runs with every lane of the wave)
+                blk_ring = 0u;
+                if (ring && chunk_minor && __builtin_amdgcn_read_exec() == ~0ull) {
+                    const uint32_t ps0 = (64u * blk_chunk) / blk_nch;
+                    const uint32_t np = (64u * blk_chunk + 63u) / blk_nch - ps0 + 1u;
+                    if (np <= P.ring_n) {
+                        if (lane < np)
+                            ring_claim(ring, ring_pos + lane, P.ring_n, P.accum, ps0 + lane,
+                                       blk_lt, (blk_ty << 16) | blk_tx, (uint32_t)P.width,
+                                       (uint32_t)P.height);
+                        __builtin_amdgcn_wave_barrier();
+                        blk_ps0 = ps0;
+                        blk_ring = ring_pos + 1u;
+                        ring_pos += np;
+                        if (ring_pos >= P.ring_n) ring_pos -= P.ring_n;
+                    }
+                }
             }
             const uint32_t avail = 64u - blk_next;
             const uint32_t mine = lanes_below(need_mask);
@@ -1515,13 +1607,19 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     g_px = px;
                     g_py = py;
                     need = false;
+                    g_ent = 0u;
+                    if (blk_ring) {  // the pixel's ring entry (+ 1)
+                        uint32_t ei = blk_ring + (slot - blk_ps0);
+                        if (ei > P.ring_n) ei -= P.ring_n;
+                        g_ent = ei;
+                    }
                 }
             }
             blk_next += min((uint32_t)__popcll(need_mask), avail);
             need_mask = __ballot(need && !done);
         }
         if (got) {
-            q = g_lt * 64u + g_slot;
+            q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
             // shader.comp:43  pixel00 + x*delta_u + y*delta_v
             acc = mk(0.f, 0.f, 0.f);
@@ -1558,7 +1656,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             if constexpr (kStats) t_cam = ticks();
             uint32_t inf = 15u;
             if (fresh && P.prim_info != nullptr)  // the sphere list of the item's 4x4 quarter
-                inf = P.prim_info[2u * ((q >> 6) * 4u + (((q >> 5) & 1u) << 1) + ((q >> 2) & 1u)) +
+                inf = P.prim_info[2u * (((q & kQMask) >> 6) * 4u + (((q >> 5) & 1u) << 1) +
+                                        ((q >> 2) & 1u)) +
                                   1u];
             const float aa = dot(d, d);
             const bool cam_now = fresh && (inf & 15u) != 15u && (P.flags & kFlagSceneBounded) != 0 &&
@@ -1668,7 +1767,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                                         lane_cnt);
                 else if constexpr (kFlat)
                     scan_culled_flat<kStats, kFmt, kGRec, kChunks, kNS>(
-                        P, tbound, tnode, tg, ws, o, d, pass == 0, q, max_t, best, w_groups,
+                        P, tbound, tnode, tg, ws, o, d, pass == 0, q & kQMask, max_t, best, w_groups,
                         w_bounds, pt);
                 else
                     scan_culled_lane<kStats>(P, tbound, tgroup, o, d, max_t, best, w_groups,
@@ -1723,6 +1822,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         atomicAdd(P.debug + 11, t_drained_rt >> 8);
     }
 #endif
+    if (ring) {  // the wave's remaining partial sums (every lane of the wave is here)
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < P.ring_n; i += 64u) ring_flush(ring[i], P.accum);
+    }
     // one segment-counter atomic per wave
     unsigned long long total = segs;  // widened before the wave sum
 #pragma unroll

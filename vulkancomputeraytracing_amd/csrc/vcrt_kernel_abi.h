@@ -81,12 +81,19 @@ struct TraceParams {
     uint32_t flags;        // kFlag*
     float spp_total;       // kFlagDirect: the divisor (samples per pixel)
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
+    // Per-wave accumulation ring in LDS (tracer.hip "Accumulation ring"): ring_n entries of 32 B
+    // per wave (0: none; <= kRingMaxEntries) at byte ring_off of the dynamic LDS, wave w of the
+    // workgroup at ring_off + 32 ring_n w. Needs local pixels < 2^kRingQBits.
+    uint32_t ring_off, ring_n;
 };
+
+constexpr uint32_t kRingMaxEntries = 63;  // entry + 1 in the top 6 bits of a lane's pixel index
+constexpr uint32_t kRingQBits = 26;
 
 constexpr int32_t kFlatMaxGroups = 1024;   // CULL_FLAT 16-bit entries: 10-bit group / node fields
 constexpr int32_t kFlatMaxGroups8 = 256;   // the LDS-table kernel: 8-bit fields, 16-bit candidates
 constexpr uint32_t kWaveScratchBytes = 4352;   // CULL_FLAT per-wave LDS stacks, 16-bit entries
-constexpr uint32_t kWaveScratchBytes8 = 3712;  // the same with 16-bit candidate entries
+constexpr uint32_t kWaveScratchBytes8 = 3456;  // 16-bit candidates, no chunk stack (LDS tables)
 constexpr uint32_t kWaveScratchBytesWide = 6912;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
