@@ -202,15 +202,16 @@ def test_groups_partition_the_scene(name):
     extent = np.linalg.norm(c.max(0) - c.min(0))
     huge = max(8 * np.partition(r, len(r) // 2)[len(r) // 2], 0.05 * extent)
     big = set(np.nonzero(r > huge)[0].tolist())
-    # ... plus, when the rest would exceed the flat scans' 1024 16-bit groups by no more than the
-    # big list's free slots, the largest of the rest (ties by index): the stress scene's 4099
-    # others -> the big three join the ground
-    rest = len(sp) - len(big)
-    if rest > 4096 and rest - 4096 <= (4 - len(big) % 4) % 4:
+    # ... plus the largest of the rest (ties by index) in the big list's free slots: the big
+    # three join the ground in both scenes
+    free = (4 - len(big) % 4) % 4
+    if big and free:
         others = [i for i in np.argsort(-r, kind="stable").tolist() if i not in big]
-        big |= set(others[:rest - 4096])
+        big |= set(others[:free])
     if name == "stress4096":
         assert big == {4096, 4097, 4098, 4099} and G == 1024
+    else:
+        assert big == {481, 482, 483, 484}
     bi = t["index"][:nb].reshape(-1)
     assert set(bi[bi >= 0].tolist()) == big
     g = t["geom"]
@@ -430,8 +431,9 @@ def test_primary_lists_hold_every_camera_ray_candidate(name, w, h, world, rank, 
         missing = may & ~inlist[None, :, None]
         assert not missing.any(), f"entry {e}: {int(missing.sum())} candidates not listed"
         total_may += int(may.sum())
-        if cnt[e]:  # control: without its last group the list would miss candidates
-            inlist[ids[-1]] = False
+        needed = [g for g in ids if may[:, g].any()]
+        if needed:  # control: without a listed group that holds candidates, the check fails
+            inlist[needed[-1]] = False
             control_hits += bool((may & ~inlist[None, :, None]).any())
     assert total_may > 0 and control_hits > 0
 

@@ -15,6 +15,8 @@ for name, k in (("scan", 8), ("big list", 15), ("levels", 9), ("node pushes", 16
                 ("node passes", 10), ("group passes", 11), ("cand passes", 12),
                 ("shade+sky", 17), ("block fetch", 18), ("camera trace", 23)):
     print("%-13s %5.1f%% of wave time, %8.1f ticks per wave-iter" % (name, 100 * d[k] / tot, d[k] / wi))
+if d[3]:
+    print("  of which shading %5.1f%% of wave time, %8.1f ticks per wave-iter" % (100 * d[3] / tot, d[3] / wi))
 print("cand passes per wave-iter %.2f; node %.2f group %.2f (from counters)" % (
     d[13] / wi, (st["bound_tests"] / wi), st["group_tests"] / wi))
 print("total ticks per wave-iter %.1f" % (tot / wi))

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 
 namespace vcrt {
@@ -147,18 +148,21 @@ bool build_cull_tables(const vcrt_sphere* s, int32_t count, CullTables& out) {
         big.resize(64);
         std::sort(big.begin(), big.end());
     }
-    // The flat scans' 16-bit stack entries address up to kFlatGroups16 hierarchy groups. When the
-    // hierarchy would exceed that by no more than the free slots of the big list's last group
-    // (the stress scene: 4096 random spheres + the big three), the largest of the rest fill
-    // those slots (ties by index): every ray tests them anyway as part of that group.
+    // The big list's last group has free slots when the big spheres are not a multiple of four;
+    // the largest of the rest fill them (ties by index). Every ray tests that group's members
+    // anyway, while in the hierarchy a large sphere inflates the boxes of its group, node and
+    // chunk for every ray that passes near it: the final scene's big three (radius 1, beside 480
+    // of radius 0.2) join the ground, C4 +9% (same bits). It also keeps the stress scene's
+    // hierarchy (4096 random spheres) within the flat scans' 1024 16-bit groups.
+    // VCRT_BIG_FILL=0 disables it (A/B).
     const size_t free_slots = (4 - big.size() % 4) % 4;
-    if (!big.empty() && normal.size() > 4 * kFlatGroups16 &&
-        normal.size() - 4 * kFlatGroups16 <= free_slots) {
+    const char* fill_env = std::getenv("VCRT_BIG_FILL");
+    const bool fill = !(fill_env && std::atoi(fill_env) == 0);
+    if (fill && !big.empty() && free_slots > 0 && normal.size() > free_slots) {
         std::stable_sort(normal.begin(), normal.end(),
                          [&](int32_t x, int32_t y) { return radii[x] > radii[y]; });
-        const size_t move = normal.size() - 4 * kFlatGroups16;
-        big.insert(big.end(), normal.begin(), normal.begin() + move);
-        normal.erase(normal.begin(), normal.begin() + move);
+        big.insert(big.end(), normal.begin(), normal.begin() + free_slots);
+        normal.erase(normal.begin(), normal.begin() + free_slots);
         std::sort(big.begin(), big.end());
         std::sort(normal.begin(), normal.end());
     }

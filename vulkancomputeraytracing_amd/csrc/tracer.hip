@@ -1742,8 +1742,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 bst = pend_best;
                 pend_best = -1;
             }
+            uint64_t t_cs = 0;
+            if constexpr (kStats) t_cs = ticks();
             if (cam_now || pending) fresh = shade_and_advance(mt, bst);
-            if constexpr (kStats) pt.cam += ticks() - t_cam;
+            if constexpr (kStats) {
+                const uint64_t t1 = ticks();
+                pt.cam += t1 - t_cam;
+                st_fetch += t1 - t_cs;  // flat stats: debug[3] = the camera phase's shading
+            }
             if (need) continue;  // that segment finished the lane's chunk
         }
 
@@ -1776,7 +1782,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
                     for (int off = 32; off > 0; off >>= 1)
                         lane_cnt = max(lane_cnt, (uint32_t)__shfl_xor((int)lane_cnt, off));
-                    st_fetch += lane_cnt;
+                    if constexpr (!kFlat) st_fetch += lane_cnt;
                 }
             } else {
                 scan_spheres<false>(P, lds_geom, n, o, d, max_t, best, hit_groups);
