@@ -412,8 +412,7 @@ __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay&
     const float4 q0 = rec[0], q1 = rec[1], idf = rec[4];
     v2f hb01, cc01, d01, hb23 = {0.f, 0.f}, cc23 = {0.f, 0.f}, d23 = {-1.f, -1.f};
     pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
-    // members 2 and 3 only when the group has them (wave-uniform; the big list of the final
-    // scene is the ground alone)
+    // members 2 and 3 only when the group has them (wave-uniform)
     if (__float_as_int(idf.z) >= 0 || __float_as_int(idf.w) >= 0)
         pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, rec[2], rec[3], hb23, cc23, d23);
     const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
