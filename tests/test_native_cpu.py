@@ -185,7 +185,8 @@ def test_work_chunk_rule(w, h, spp):
     """vcrt_work_chunk (the accumulation chunk vcrt_begin uses; host only): the same for every
     rank of a sharded frame, at most spp, at most 512 chunks per pixel, >= 4 unless spp is
     smaller, and an explicit accumulate_chunk is taken as given. Checked against the rule
-    restated here (64, halved while the largest rank has < 2^24 - 2^21 items)."""
+    restated here (64, halved while the largest rank has < 2^24 - 2^21 items, down to 16, or to
+    32 for frames of fewer than 2^22 items at 32)."""
     for world in (1, 2, 3, 8):
         ks = {vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
                                                    rank=rank, world_size=world))
@@ -197,7 +198,8 @@ def test_work_chunk_rule(w, h, spp):
         assert k == spp or k >= 16
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
         want = 64
-        while want > 16 and slots * -(-spp // want) < (1 << 24) - (1 << 21):
+        floor = 32 if slots * -(-spp // 32) < (1 << 22) else 16  # small frames stop at 32
+        while want > floor and slots * -(-spp // want) < (1 << 24) - (1 << 21):
             want //= 2
         assert k == min(max(want, -(-spp // 512)), spp)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
