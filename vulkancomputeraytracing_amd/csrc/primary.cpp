@@ -20,8 +20,10 @@
 // against fp32 emulations of the kernel's camera rays and discriminants.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <thread>
 
 #include "cluster.hpp"
 #include "vcrt_math.h"
@@ -176,6 +178,24 @@ struct QuarterWalker {
     }
 };
 
+// Runs body(begin, end, part) over [0, n) in contiguous parts on up to 16 host threads
+// (VCRT_HOST_THREADS overrides; parts of at least 2048 quarters); part p covers a range after
+// part p - 1's, so concatenating per-part outputs in part order gives the serial result.
+template <typename Body>
+uint32_t parallel_parts(uint32_t n, Body&& body) {
+    uint32_t threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("VCRT_HOST_THREADS"))
+        threads = static_cast<uint32_t>(std::min(16, std::max(1, std::atoi(e))));
+    const uint32_t parts = std::max(1u, std::min(threads, (n + 2047) / 2048));
+    const uint32_t per = (n + parts - 1) / parts;
+    std::vector<std::thread> pool;
+    for (uint32_t t = 1; t < parts; t++)
+        pool.emplace_back([&, t] { body(std::min(n, t * per), std::min(n, (t + 1) * per), t); });
+    body(0, std::min(n, per), 0u);
+    for (auto& th : pool) th.join();
+    return parts;
+}
+
 }  // namespace
 
 void build_primary_lists(const CullTables& ct, const float cam[12], int32_t width,
@@ -184,15 +204,33 @@ void build_primary_lists(const CullTables& ct, const float cam[12], int32_t widt
     out.ids.clear();
     const QuarterWalker qw(ct, cam, width, height, rank, world);
     const size_t ng = static_cast<size_t>(ct.ngroups);
-    out.info.assign(4 * qw.nloc, kPrimaryNone);
-    std::vector<uint32_t> found;
-    for (uint32_t e = 0; e < 4 * qw.nloc; e++) {
-        const bool fits = qw.groups(qw.pyramid(e), kPrimaryMax, found);
-        const size_t cnt = found.size();
-        // ids are uint16 and offsets 28-bit: beyond that the quarter keeps no list
-        if (!fits || ng > 0xFFFFu || out.ids.size() + cnt >= (size_t{1} << 28)) continue;
-        out.info[e] = static_cast<uint32_t>(out.ids.size()) << 4 | static_cast<uint32_t>(cnt);
-        for (uint32_t g : found) out.ids.push_back(static_cast<uint16_t>(g));
+    const uint32_t n = 4 * qw.nloc;
+    out.info.assign(n, kPrimaryNone);
+    // per part: its quarters' group ids, offsets relative to the part (fixed up below)
+    std::vector<std::vector<uint16_t>> ids(16);
+    const uint32_t parts = parallel_parts(n, [&](uint32_t b, uint32_t e_end, uint32_t part) {
+        std::vector<uint32_t> found;
+        std::vector<uint16_t>& mine = ids[part];
+        for (uint32_t e = b; e < e_end; e++) {
+            const bool fits = qw.groups(qw.pyramid(e), kPrimaryMax, found);
+            const size_t cnt = found.size();
+            if (!fits || ng > 0xFFFFu) continue;  // ids are uint16
+            out.info[e] = static_cast<uint32_t>(mine.size()) << 4 | static_cast<uint32_t>(cnt);
+            for (uint32_t g : found) mine.push_back(static_cast<uint16_t>(g));
+        }
+    });
+    // concatenate in part order; offsets are 28-bit: beyond that a quarter keeps no list
+    const uint32_t per = (n + parts - 1) / parts;
+    for (uint32_t part = 0; part < parts; part++) {
+        const size_t base = out.ids.size();
+        for (uint32_t e = part * per; e < std::min(n, (part + 1) * per); e++) {
+            if (out.info[e] == kPrimaryNone) continue;
+            const size_t off = base + (out.info[e] >> 4);
+            out.info[e] = off + (out.info[e] & 15u) >= (size_t{1} << 28)
+                              ? kPrimaryNone
+                              : static_cast<uint32_t>(off) << 4 | (out.info[e] & 15u);
+        }
+        out.ids.insert(out.ids.end(), ids[part].begin(), ids[part].end());
     }
 }
 
@@ -202,57 +240,75 @@ void build_primary_sphere_lists(const CullTables& ct, const vcrt_sphere* spheres
     out.info.clear();
     out.rec.clear();
     const QuarterWalker qw(ct, cam, width, height, rank, world);
-    out.info.assign(4 * qw.nloc, kPrimaryNone);
+    const uint32_t n = 4 * qw.nloc;
+    out.info.assign(n, kPrimaryNone);
     const float ox = cam[9], oy = cam[10], oz = cam[11];
-    std::vector<uint32_t> found;
-    std::vector<int32_t> members;
-    for (uint32_t e = 0; e < 4 * qw.nloc; e++) {
-        const Pyramid P = qw.pyramid(e);
-        // the group walk bounds the work; a quarter meeting very many groups keeps no list
-        if (!qw.groups(P, 64, found)) continue;
-        members.clear();
-        bool over = false;
-        for (uint32_t gi : found) {
-            for (int k = 0; k < 4 && !over; k++) {
-                const int32_t j = ct.index[(ct.nbig + gi) * 4 + k];
-                if (j < 0) continue;
-                const vcrt_sphere& sp = spheres[j];
-                const double c[3] = {sp.center[0], sp.center[1], sp.center[2]};
-                const double r = std::fabs(static_cast<double>(sp.radius));
-                double oc2 = 0.0;
-                for (int a = 0; a < 3; a++) oc2 += (qw.o[a] - c[a]) * (qw.o[a] - c[a]);
-                // the member's own margin (tracer.hip fact (2)), and the rounding of the rays
-                const double Ms = r > 0.0 ? 8.1 * 0x1p-24 * (oc2 + r * r) / r * (1.0 + 1e-5)
-                                          : std::numeric_limits<double>::infinity();
-                if (!(Ms < 1e30) || !sphere_outside(P, c, r + Ms + QuarterWalker::kExtra)) {
-                    if (members.size() == kPrimarySphereMax) over = true;
-                    else members.push_back(j);
+    // per part: its quarters' pair records, first pair relative to the part (fixed up below)
+    std::vector<std::vector<float>> recs(16);
+    const uint32_t parts = parallel_parts(n, [&](uint32_t b, uint32_t e_end, uint32_t part) {
+        std::vector<uint32_t> found;
+        std::vector<int32_t> members;
+        std::vector<float>& mine = recs[part];
+        for (uint32_t e = b; e < e_end; e++) {
+            const Pyramid P = qw.pyramid(e);
+            // the group walk bounds the work; a quarter meeting very many groups keeps no list
+            if (!qw.groups(P, 64, found)) continue;
+            members.clear();
+            bool over = false;
+            for (uint32_t gi : found) {
+                for (int k = 0; k < 4 && !over; k++) {
+                    const int32_t j = ct.index[(ct.nbig + gi) * 4 + k];
+                    if (j < 0) continue;
+                    const vcrt_sphere& sp = spheres[j];
+                    const double c[3] = {sp.center[0], sp.center[1], sp.center[2]};
+                    const double r = std::fabs(static_cast<double>(sp.radius));
+                    double oc2 = 0.0;
+                    for (int a = 0; a < 3; a++) oc2 += (qw.o[a] - c[a]) * (qw.o[a] - c[a]);
+                    // the member's own margin (tracer.hip fact (2)), and the rounding of the rays
+                    const double Ms = r > 0.0 ? 8.1 * 0x1p-24 * (oc2 + r * r) / r * (1.0 + 1e-5)
+                                              : std::numeric_limits<double>::infinity();
+                    if (!(Ms < 1e30) || !sphere_outside(P, c, r + Ms + QuarterWalker::kExtra)) {
+                        if (members.size() == kPrimarySphereMax) over = true;
+                        else members.push_back(j);
+                    }
                 }
             }
-        }
-        if (over) continue;
-        const size_t first = out.rec.size() / 12;
-        if (first >= (size_t{1} << 28)) continue;
-        out.info[e] = static_cast<uint32_t>(first) << 4 | static_cast<uint32_t>(members.size());
-        for (size_t m = 0; m < members.size(); m += 2) {
-            float r[12] = {0, 0, 0, 0, 0, 0, 3.0e38f, 3.0e38f, 0, 0, 0, 0};
-            int32_t idx[2] = {-1, -1};
-            for (int e2 = 0; e2 < 2 && m + e2 < members.size(); e2++) {
-                const vcrt_sphere& sp = spheres[members[m + e2]];
-                // pair_disc_cc's operations and order: oc = o - c, cc = ((ocx ocx + ocy ocy) +
-                // ocz ocz) - r^2 with r^2 = radius * radius, fp32, no FMA
-                const float ocx = ox - sp.center[0], ocy = oy - sp.center[1],
-                            ocz = oz - sp.center[2];
-                const float r2 = sp.radius * sp.radius;
-                r[0 + e2] = ocx;
-                r[2 + e2] = ocy;
-                r[4 + e2] = ocz;
-                r[6 + e2] = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
-                idx[e2] = members[m + e2];
+            if (over) continue;
+            out.info[e] = static_cast<uint32_t>(mine.size() / 12) << 4 |
+                          static_cast<uint32_t>(members.size());
+            for (size_t m = 0; m < members.size(); m += 2) {
+                float r[12] = {0, 0, 0, 0, 0, 0, 3.0e38f, 3.0e38f, 0, 0, 0, 0};
+                int32_t idx[2] = {-1, -1};
+                for (int e2 = 0; e2 < 2 && m + e2 < members.size(); e2++) {
+                    const vcrt_sphere& sp = spheres[members[m + e2]];
+                    // pair_disc_cc's operations and order: oc = o - c, cc = ((ocx ocx + ocy ocy)
+                    // + ocz ocz) - r^2 with r^2 = radius * radius, fp32, no FMA
+                    const float ocx = ox - sp.center[0], ocy = oy - sp.center[1],
+                                ocz = oz - sp.center[2];
+                    const float r2 = sp.radius * sp.radius;
+                    r[0 + e2] = ocx;
+                    r[2 + e2] = ocy;
+                    r[4 + e2] = ocz;
+                    r[6 + e2] = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
+                    idx[e2] = members[m + e2];
+                }
+                std::memcpy(&r[8], idx, sizeof(idx));
+                mine.insert(mine.end(), r, r + 12);
             }
-            std::memcpy(&r[8], idx, sizeof(idx));
-            out.rec.insert(out.rec.end(), r, r + 12);
         }
+    });
+    // concatenate in part order; first pairs are 28-bit: beyond that a quarter keeps no list
+    const uint32_t per = (n + parts - 1) / parts;
+    for (uint32_t part = 0; part < parts; part++) {
+        const size_t base = out.rec.size() / 12;
+        for (uint32_t e = part * per; e < std::min(n, (part + 1) * per); e++) {
+            if (out.info[e] == kPrimaryNone) continue;
+            const size_t first = base + (out.info[e] >> 4);
+            out.info[e] = first >= (size_t{1} << 28)
+                              ? kPrimaryNone
+                              : static_cast<uint32_t>(first) << 4 | (out.info[e] & 15u);
+        }
+        out.rec.insert(out.rec.end(), recs[part].begin(), recs[part].end());
     }
 }
 
