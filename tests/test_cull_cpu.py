@@ -5,7 +5,10 @@ table's values, and (2) a group whose box test rules it out for a ray holds no s
 fp32 discriminant (hit_sphere, functions.glsl:14-22, as tracer.hip's pair_disc evaluates it) is
 >= 0. (2) is checked here by emulating both fp32 evaluations in numpy on random rays (near and
 far origins), on rays built to graze member spheres within 1e-7..1e-4 of their radius, and on
-rays grazing a member where it touches its box.
+rays grazing a member where it touches its box. The kernels also rule out a box whose stretch of
+the ray's line lies behind -tau (tracer.hip fact (4)): there the property is that a ruled-out box
+holds no member the exact test may accept (disc >= 0 and hb or cc negative), checked on rays
+leaving member spheres' surfaces and on rays just past a member, pointing away from it.
 """
 import numpy as np
 import pytest
@@ -37,25 +40,37 @@ def ulp_noise(x, rng, ulps=1):
     return out.astype(f32)
 
 
-def box_ray(t, o, d, rng=None):
-    """tracer.hip box_ray in fp32: per axis inv = v_rcp(d'), c = -o inv; c1, c2."""
+CLIP = True  # tracer.hip VCRT_BOX_CLIP: fact (4), the near end clamped at -tau
+
+
+def box_ray(t, o, d, rng=None, tau_scale=1.0):
+    """tracer.hip box_ray in fp32: per axis inv = v_rcp(d'), c = fma(-o, inv, tau) with
+    tau = sqrt(3.2e-7 Q / a) (fact (4); tau_scale scales it for the checker's own test); c1, c2."""
     cmax, rmax2, lam = (f32(v) for v in t["margin"][:3])
     dd = np.where(np.abs(d) < f32(2.0 ** -40), np.copysign(f32(2.0 ** -40), d), d).astype(f32)
     inv = ulp_noise(rn(1.0 / dd.astype(np.float64)), rng)
-    c = rn(-o.astype(np.float64) * inv)
-    J = rn(f32(2.002) * np.abs(inv).max(1))
     dot = rn(rn(rn(o[:, 0] * o[:, 0]) + rn(o[:, 1] * o[:, 1])) + rn(o[:, 2] * o[:, 2]))
     on = rn(ulp_noise(rn(np.sqrt(dot.astype(np.float64))), rng) + cmax)
     Q = rn(rn(on * on) + rmax2)
+    tau = np.zeros(len(o), f32)
+    if CLIP:
+        a = rn(rn(rn(d[:, 0] * d[:, 0]) + rn(d[:, 1] * d[:, 1])) + rn(d[:, 2] * d[:, 2]))
+        with np.errstate(divide="ignore", over="ignore"):
+            ya = ulp_noise(rn(1.0 / a.astype(np.float64)), rng)
+            arg = rn(rn(f32(3.2e-7) * Q) * ya)
+        tau = ulp_noise(rn(np.sqrt(arg.astype(np.float64))), rng)
+        tau = rn(tau.astype(np.float64) * tau_scale)
+    c = fma(-o, inv, np.broadcast_to(tau[:, None], inv.shape))
+    J = rn(f32(2.002) * np.abs(inv).max(1))
     oinf = np.abs(o).max(1)
     c1 = rn(J * rn(f32(3.04e-7) * rn(lam + oinf)))
     c2 = rn(J * Q)
     return inv, c, c1, c2
 
 
-def group_culled(t, o, d, key="bound", rng=None):
-    """[rays, boxes] bool: the kernel's box test (tracer.hip box_gap, fact (3)) on the group
-    boxes (key "bound"), the node boxes ("node") or the chunk boxes ("top"), in fp32 with
+def group_culled(t, o, d, key="bound", rng=None, tau_scale=1.0):
+    """[rays, boxes] bool: the kernel's box test (tracer.hip box_gap, facts (3) and (4)) on the
+    group boxes (key "bound"), the node boxes ("node") or the chunk boxes ("top"), in fp32 with
     v_rcp_f32 / v_sqrt_f32's 1-ulp errors emulated by random perturbations (rng)."""
     b = t[key]
     G = 2 * b.shape[0]
@@ -63,7 +78,7 @@ def group_culled(t, o, d, key="bound", rng=None):
     lo = [cols(0), cols(2), cols(4)]
     hi = [cols(6), cols(8), cols(10)]
     K = cols(12)
-    inv, c, c1, c2 = box_ray(t, o, d, rng)
+    inv, c, c1, c2 = box_ray(t, o, d, rng, tau_scale)
     tn = tf = None
     for k in range(3):
         tl = fma(lo[k][None, :], inv[:, k, None], c[:, k, None])
@@ -71,6 +86,8 @@ def group_culled(t, o, d, key="bound", rng=None):
         near, far = np.minimum(tl, th), np.maximum(tl, th)
         tn = near if tn is None else np.maximum(tn, near)
         tf = far if tf is None else np.minimum(tf, far)
+    if CLIP:
+        tn = np.maximum(tn, f32(0))
     with np.errstate(over="ignore", invalid="ignore"):
         gap = fma(np.broadcast_to(K[None, :], tn.shape), np.broadcast_to(c2[:, None], tn.shape),
                   rn(rn(tf - tn) + c1[:, None]))
@@ -98,6 +115,8 @@ def group_gap(t, o, d, key="bound", near_far=False):
             near, far = np.minimum(tl, th), np.maximum(tl, th)
         tn = near if tn is None else np.maximum(tn, near)
         tf = far if tf is None else np.minimum(tf, far)
+    if CLIP:
+        tn = np.maximum(tn, f32(0))
     with np.errstate(over="ignore", invalid="ignore"):
         return fma(np.broadcast_to(K[None, :], tn.shape), np.broadcast_to(c2[:, None], tn.shape),
                    rn(rn(tf - tn) + c1[:, None]))
@@ -176,6 +195,25 @@ def tangent_rays(spheres, t, n, rng):
         os_.append(q - rng.uniform(0.5, 40.0) * p)
         ds_.append(p * rng.choice([0.01, 1.0, 100.0]))
     return np.array(os_, f32), np.array(ds_, f32)
+
+
+def surface_rays(spheres, n, rng):
+    """Secondary rays: origins on member spheres' surfaces (rounded to fp32, so just inside or
+    outside), directions normal + a random unit vector (scattered) or random (refracted), and
+    rays just past a member (0..1e-3 of its radius beyond the surface) pointing away from it."""
+    idx = rng.integers(0, len(spheres), n)
+    c = spheres["center"][idx].astype(np.float64)
+    r = np.abs(spheres["radius"][idx].astype(np.float64))
+    nrm = rng.normal(size=(n, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    gap = rng.choice([0.0, 0.0, 1e-7, 1e-5, 1e-3], n)[:, None]
+    o = c + nrm * (r[:, None] * (1 + gap))
+    kind = rng.integers(0, 3, n)[:, None]
+    d = np.where(kind == 0, nrm + u, np.where(kind == 1, u, nrm + 0.05 * u))
+    d *= rng.choice([0.05, 1.0, 3.0], n)[:, None]
+    return o.astype(f32), d.astype(f32)
 
 
 def random_rays(n, rng, lo, hi):
@@ -258,20 +296,22 @@ def test_bound_test_is_conservative(name):
     chunks += [tangent_rays(sp, t, 1500, rng) for _ in range(2)]
     chunks += [random_rays(1500, rng, -20.0, 20.0), random_rays(500, rng, -2.0, 2.0)]
     chunks += [random_rays(500, rng, -3000.0, 3000.0)]  # far origins: large margins
+    chunks += [surface_rays(sp, 1500, rng) for _ in range(2)]
     for o, d in chunks:
         culled = group_culled(t, o, d, rng=rng)
-        disc = member_disc(t, o, d)
-        hit = (~(disc < 0)) & valid[None]
+        hb, cc, disc = member_hb_cc_disc(t, o, d)
+        # members the exact test may accept (may_hit / hit_sign: -0 counts as negative)
+        hit = (~(disc < 0)) & (np.signbit(hb) | np.signbit(cc)) & valid[None]
         bad = culled[:, :, None] & hit
-        assert not bad.any(), f"{int(bad.sum())} culled group members with disc >= 0"
-        # a culled node (8 consecutive groups) holds no hit either
+        assert not bad.any(), f"{int(bad.sum())} culled group members that may be accepted"
+        # a culled node (8 consecutive groups) holds no such member either
         node_culled = np.repeat(group_culled(t, o, d, "node", rng=rng), 8, axis=1)
         bad = node_culled[:, :, None] & hit
-        assert not bad.any(), f"{int(bad.sum())} culled node members with disc >= 0"
+        assert not bad.any(), f"{int(bad.sum())} culled node members that may be accepted"
         G = hit.shape[1]
         top_culled = np.repeat(group_culled(t, o, d, "top", rng=rng), 64, axis=1)[:, :G]
         bad = top_culled[:, :, None] & hit
-        assert not bad.any(), f"{int(bad.sum())} culled top-level members with disc >= 0"
+        assert not bad.any(), f"{int(bad.sum())} culled top-level members that may be accepted"
         total_culled += int(culled.sum())
         total += culled.size
     # and the test does cull (most groups are far from most rays)
@@ -297,6 +337,30 @@ def test_checker_detects_a_too_small_box():
     culled = group_culled(bad_t, o, d)
     hit = ~(member_disc(t, o, d) < 0) & (t["index"][t["nbig"]:] >= 0)[None]
     assert (culled[:, :, None] & hit).any()
+
+
+@pytest.mark.parametrize("name", ["final", "stress4096"])
+def test_clip_behind_origin_culls_and_has_teeth(name):
+    """Fact (4) rules out boxes the line test keeps (secondary rays leave a sphere: about half
+    the boxes their line crosses lie behind the origin), and the check above would catch a clip
+    that reached past -tau: planes shifted by -50 tau (the clamp then cuts the line ahead of the
+    origin) cull members the exact test may accept."""
+    global CLIP
+    rng = np.random.default_rng(5)
+    sp = S.builtin_scene(name)
+    t = S.cull_tables(sp)
+    valid = t["index"][t["nbig"]:] >= 0
+    o, d = surface_rays(sp, 1500, rng)
+    clipped = group_culled(t, o, d).sum()
+    try:
+        CLIP = False
+        line = group_culled(t, o, d).sum()
+    finally:
+        CLIP = True
+    assert clipped > line + 0.01 * (~group_culled(t, o, d)).sum()
+    hb, cc, disc = member_hb_cc_disc(t, o, d)
+    hit = (~(disc < 0)) & (np.signbit(hb) | np.signbit(cc)) & valid[None]
+    assert (group_culled(t, o, d, tau_scale=-50.0)[:, :, None] & hit).any()
 
 
 def test_margin_constants():

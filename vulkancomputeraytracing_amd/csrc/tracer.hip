@@ -203,7 +203,22 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
 //      roundings: gap >= 0, the box is kept. Hence a ruled-out box holds no member with
 //      disc_f >= 0. (Q and the 1.001 factors absorb the per-ray roundings; K_b = inf, a zero
 //      radius, keeps its box.) The host passes K_b, c_max, r_max^2 and L rounded up.
+//  (4) behind the origin. A member is accepted only if hb_f < 0 or cc_f < 0 (may_hit). If the
+//      line meets the member's sphere grown by M_s only at t < -tau (or not at all), with
+//      tau^2 = 5.02u Q / a, then exactly hb = -a t_c > a tau >= 4.02u |oc| |d| (t_c: the
+//      centre's parameter) and cc = |oc|^2 - r^2 > a tau^2 >= 5.02u (|oc|^2 + r^2), which
+//      the roundings of hb_f (4.02u |oc| |d|: oc and the dot) and of cc_f (5.02u |oc|^2 and u r^2)
+//      cannot flip: hb_f >= 0 and cc_f >= 0, rejected. So an accepted member's grown sphere,
+//      inside the grown box, meets the line at some t* >= -tau, and the computed far end is at
+//      least t* - (c1 + K_b c2) / 2 by (3). The kernels shift every plane by tau (c = fma(-o,
+//      inv, tau): t' = t + tau, gaps unchanged; the shift's roundings, below 4.1u tau, fit in
+//      c1's spare) and clamp the near end at 0: gap = fma(K_b, c2, (tf' - max(tn', 0)) + c1)
+//      rules a box out when its whole stretch of the line lies behind -tau as well.
+//      (tau = sqrt(3.2e-7 Q / a), 7% above 5.02u Q / a for the roundings of Q, 1/a and sqrt.)
 // Waves holding a ray outside the guarded range scan the original table in reference order.
+#ifndef VCRT_BOX_CLIP
+#define VCRT_BOX_CLIP 1  // (4): 0 = the line test alone (A/B builds)
+#endif
 
 // t of one candidate as hit_sphere would accept it (finite case, fact (1)).
 __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
@@ -339,22 +354,24 @@ struct BoxRay {
     v2f c1, c2;      // gap slack: c1 + K_b c2
 };
 
-__device__ __forceinline__ float box_axis(float o, float d, v2f& i, v2f& c) {
+__device__ __forceinline__ float box_axis(float o, float d, float tau, v2f& i, v2f& c) {
     const float dd = copysignf(fmaxf(fabsf(d), 0x1p-40f), d);
     const float iv = __builtin_amdgcn_rcpf(dd);
-    const float co = -o * iv;
+    const float co = __builtin_fmaf(-o, iv, tau);  // the plane shift of (4) (tau = 0: none)
     i = (v2f){iv, iv};
     c = (v2f){co, co};
     return fabsf(iv);
 }
 
-__device__ __forceinline__ BoxRay box_ray(const TraceParams& p, const f3 o, const f3 d) {
+// ya: recip_a(dot(d, d)), for tau of (4)
+__device__ __forceinline__ BoxRay box_ray(const TraceParams& p, const f3 o, const f3 d, float ya) {
     BoxRay r;
-    const float ax = box_axis(o.x, d.x, r.ix, r.cx), ay = box_axis(o.y, d.y, r.iy, r.cy),
-                az = box_axis(o.z, d.z, r.iz, r.cz);
-    const float J = 2.002f * fmaxf(fmaxf(ax, ay), az);  // 1.001 J
     const float on = __builtin_amdgcn_sqrtf(dot(o, o)) + p.box_margin[0];
     const float Q = on * on + p.box_margin[1];
+    const float tau = VCRT_BOX_CLIP ? __builtin_amdgcn_sqrtf(3.2e-7f * Q * ya) : 0.0f;
+    const float ax = box_axis(o.x, d.x, tau, r.ix, r.cx), ay = box_axis(o.y, d.y, tau, r.iy, r.cy),
+                az = box_axis(o.z, d.z, tau, r.iz, r.cz);
+    const float J = 2.002f * fmaxf(fmaxf(ax, ay), az);  // 1.001 J
     const float oinf = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float c1 = J * (3.04e-7f * (p.box_margin[2] + oinf));  // 5.1u
     const float c2 = J * Q;
@@ -378,6 +395,10 @@ __device__ __forceinline__ v2f box_gap(const BoxRay& r, float4 b0, float4 b1, fl
     tn.y = fmaxf(fmaxf(fminf(tlx.y, thx.y), fminf(tly.y, thy.y)), fminf(tlz.y, thz.y));
     tf.x = fminf(fminf(fmaxf(tlx.x, thx.x), fmaxf(tly.x, thy.x)), fmaxf(tlz.x, thz.x));
     tf.y = fminf(fminf(fmaxf(tlx.y, thx.y), fmaxf(tly.y, thy.y)), fmaxf(tlz.y, thz.y));
+    if (VCRT_BOX_CLIP) {  // (4): the stretch of the line behind -tau does not count
+        tn.x = fmaxf(tn.x, 0.0f);
+        tn.y = fmaxf(tn.y, 0.0f);
+    }
     return vfma(K, r.c2, (tf - tn) + r.c1);
 }
 
@@ -464,7 +485,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     r.ox = (v2f){o.x, o.x};
     r.oy = (v2f){o.y, o.y};
     r.oz = (v2f){o.z, o.z};
-    const BoxRay br = box_ray(p, o, d);
+    const BoxRay br = box_ray(p, o, d, recip_a(a));
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     cfloat4* bound = (cfloat4*)p.cbound;
     cfloat4* node = (cfloat4*)p.cnode;
@@ -611,6 +632,10 @@ __device__ __forceinline__ uint32_t push_bound_pair_nf(uint32_t acc, const BoxRa
     tn.y = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
     tf.x = fminf(fminf(tfx.x, tfy.x), tfz.x);
     tf.y = fminf(fminf(tfx.y, tfy.y), tfz.y);
+    if (VCRT_BOX_CLIP) {  // (4), as box_gap
+        tn.x = fmaxf(tn.x, 0.0f);
+        tn.y = fmaxf(tn.y, 0.0f);
+    }
     const v2f D = vfma(ld2(a.k + off), r.c2, (tf - tn) + r.c1);
     return push_sign(push_sign(acc, D.y), D.x);
 }
@@ -972,7 +997,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     my.dz = d.z;
     my.a = dot(d, d);
     my.ya = recip_a(my.a);
-    my.br = box_ray(p, o, d);
+    my.br = box_ray(p, o, d, my.ya);
     const BoxRay& br = my.br;
     CullRay r;
     r.ox = (v2f){o.x, o.x};
@@ -1090,7 +1115,7 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
     r.ox = (v2f){o.x, o.x};
     r.oy = (v2f){o.y, o.y};
     r.oz = (v2f){o.z, o.z};
-    const BoxRay br = box_ray(p, o, d);
+    const BoxRay br = box_ray(p, o, d, recip_a(a));
     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {a, a};
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* top = (cfloat4*)p.ctop;
