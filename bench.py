@@ -26,8 +26,9 @@ PEAK_FP32_NONFMA_TFLOPS = 78.65  # the same issue rate without FMA (1 flop per l
                                  # add/mul): the ceiling of the exact sphere test, which parity
                                  # keeps free of contraction
 FLOPS_PER_SPHERE_TEST = 23      # functions.glsl:15-19 as written
-FLOPS_PER_BOUND_TEST = 26       # tracer.hip box_gap, per box: 6 fma 12, per-axis min/max 6,
-                                # tnear/tfar 4, gap sub + add + fma 4
+FLOPS_PER_BOUND_TEST = 27       # tracer.hip box_gap, per box: 6 fma 12, per-axis min/max 6,
+                                # tnear/tfar 4, the near end's clamp at 0 (fact (4)) 1,
+                                # gap sub + add + fma 4
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic.json")
 
 

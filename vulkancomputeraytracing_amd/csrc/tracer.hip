@@ -48,6 +48,15 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask) {
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// Issued-work tallies (TraceParams.work_done): a wave-uniform count x is credited to the wave's
+// first active lane, so the sum over the lanes is the wave's total. (A per-wave 64-bit counter
+// is per lane under SIMT all the same -- lanes that skip a region keep their old value -- and
+// lived in VGPR pairs that spilled, with a full vmcnt wait at every update.)
+__device__ __forceinline__ void tally(uint32_t& t, uint32_t x) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+    t += (threadIdx.x & 63u) == first ? x : 0u;
+}
+
 typedef __attribute__((address_space(4))) const float4 cfloat4;
 
 // One group = four spheres in pair-SoA form: q[0] = (cx0,cx1,cy0,cy1), q[1] = (cz0,cz1,r0²,r1²),
@@ -476,10 +485,11 @@ __device__ __forceinline__ void exact_group_uniform_cam(cfloat4* crec, cfloat4* 
 // and in `lane_cnt` the groups this lane needs.
 template <bool kStats>
 __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, const f3 d,
-                                            float& max_t, int& best, uint64_t& groups_tested,
-                                            uint64_t& bounds_tested, uint32_t& hit_groups,
+                                            float& max_t, int& best, uint32_t& groups_tested,
+                                            uint32_t& bounds_tested, uint32_t& hit_groups,
                                             uint32_t& lane_cnt) {
     uint32_t node_lanes = 0, node_cnt = 0;
+    uint32_t n_groups = 0, n_bounds = 0;
     const float a = dot(d, d);
     CullRay r;
     r.ox = (v2f){o.x, o.x};
@@ -492,7 +502,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
     cfloat4* geom = (cfloat4*)p.cgroup;
     for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray
         exact_group_uniform(geom + 5 * gb, r, dx, dy, dz, a2, a, recip_a(a), max_t, best);
-    groups_tested += (uint64_t)p.nbig;
+    n_groups += (uint32_t)p.nbig;
     geom += 5 * p.nbig;           // the hierarchy's groups
     const int ncg = p.ncgroups;  // multiple of 16: whole node pairs
     cfloat4* top = (cfloat4*)p.ctop;
@@ -502,7 +512,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
         if ((base & 127) == 0) {
             tops = bound_pair_need<false>(br, load_bound_pair(top + 4 * (base >> 7)), node_lanes,
                                           node_cnt);
-            bounds_tested += 2;
+            n_bounds += 2;
         }
         if (((tops >> ((base >> 6) & 1)) & 1u) == 0) continue;
         // level 1: which of the next (up to) 8 nodes of 8 groups may any lane hit? (the
@@ -516,7 +526,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
             nodes |= bound_pair_need<false>(br, cur, node_lanes, node_cnt) << j;
             cur = nxt;
         }
-        bounds_tested += (uint64_t)(nn + 8 * __popc(nodes));
+        n_bounds += (uint32_t)(nn + 8 * __popc(nodes));
         // level 2: which groups of those nodes?
         uint64_t need = 0;
         if (nodes) cur = load_bound_pair(bound + 4 * ((base + 8 * __builtin_ctz(nodes)) >> 1));
@@ -534,7 +544,7 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
             }
         }
         // the exact hit_sphere test on the groups that survived (next group prefetched)
-        groups_tested += (uint64_t)__popcll(need);
+        n_groups += (uint32_t)__popcll(need);
         if (!need) continue;
         int gi = base + __builtin_ctzll(need);
         float4 q0 = geom[5 * gi], q1 = geom[5 * gi + 1], q2 = geom[5 * gi + 2],
@@ -569,6 +579,8 @@ __device__ __forceinline__ void scan_culled(const TraceParams& p, const f3 o, co
             q3 = n3;
         }
     }
+    tally(groups_tested, 2u * n_groups);  // in half-groups
+    tally(bounds_tested, n_bounds);
 }
 
 // Per-lane culled scan (variant CULL_LANE). Same tables and tests as scan_culled, but only
@@ -980,7 +992,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                                                  const GroupTab<kGRec>& tg, WS* ws,
                                                  const f3 o, const f3 d, bool primary,
                                                  uint32_t item, float& max_t, int& best,
-                                                 uint64_t& groups_tested, uint64_t& bounds_tested,
+                                                 uint32_t& groups_tested, uint32_t& bounds_tested,
                                                  PhaseTicks& pt) {
     uint64_t t_in = 0;
     if constexpr (kStats) t_in = ticks();
@@ -1099,16 +1111,16 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     const unsigned long long k = ws->key[lane];
     max_t = __uint_as_float((uint32_t)(k >> 32));
     best = (int)(uint32_t)k;
-    bounds_tested += __builtin_amdgcn_readfirstlane(n_bounds);
-    groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
+    tally(bounds_tested, __builtin_amdgcn_readfirstlane(n_bounds));
+    tally(groups_tested, 2u * __builtin_amdgcn_readfirstlane(n_groups));  // half-groups
 }
 
 template <bool kStats>
 __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const float4* tbound,
                                                  const float4* tgroup, const f3 o, const f3 d,
                                                  float& max_t, int& best,
-                                                 uint64_t& groups_tested,
-                                                 uint64_t& bounds_tested, uint32_t& lane_cnt,
+                                                 uint32_t& groups_tested,
+                                                 uint32_t& bounds_tested, uint32_t& lane_cnt,
                                                  uint32_t& rounds) {
     const float a = dot(d, d);
     CullRay r;
@@ -1202,8 +1214,8 @@ __device__ __forceinline__ void scan_culled_lane(const TraceParams& p, const flo
             }
         }
     }
-    bounds_tested += __builtin_amdgcn_readfirstlane(n_bounds);
-    groups_tested += __builtin_amdgcn_readfirstlane(n_groups);
+    tally(bounds_tested, __builtin_amdgcn_readfirstlane(n_bounds));
+    tally(groups_tested, 2u * __builtin_amdgcn_readfirstlane(n_groups));  // half-groups
 }
 
 // ---- Accumulation ring ---------------------------------------------------------------------
@@ -1381,8 +1393,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     };
     uint32_t segs = 0;  // this lane's segments (< 2^32: ~2.4e5 per lane at the C5 workload)
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
-    uint64_t w_groups = 0, w_bounds = 0;  // per wave (uniform): sphere groups / bounds tested
-    uint32_t w_pairs = 0;                 // per wave: sphere-pair tests of the camera lists
+    // issued work (tally): half-groups (sphere-pair tests of the camera lists count one, group
+    // tests two) and box tests
+    uint32_t w_halves = 0, w_bounds = 0;
     PhaseTicks pt;                         // stats builds: wave clock per phase
     uint64_t t_begin = 0;
     if constexpr (kStats) t_begin = ticks();
@@ -1754,8 +1767,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 }
                 // issued work: the big list and the loop's passes (a pair test is half a group
                 // test), per wave
-                w_groups += (uint64_t)P.nbig;
-                w_pairs += wave_max_small<3>(iters);
+                tally(w_halves, 2u * (uint32_t)P.nbig + wave_max_small<3>(iters));
             }
             // One shading for the camera rays just traced and the main-scan hits of the last
             // iteration: the hit branches run once per iteration for both (a lane has at most
@@ -1793,14 +1805,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 uint64_t t0 = 0;
                 if constexpr (kStats) t0 = ticks();
                 if constexpr (kCull == 1)
-                    scan_culled<kStats>(P, o, d, max_t, best, w_groups, w_bounds, hit_groups,
+                    scan_culled<kStats>(P, o, d, max_t, best, w_halves, w_bounds, hit_groups,
                                         lane_cnt);
                 else if constexpr (kFlat)
                     scan_culled_flat<kStats, kFmt, kGRec, kChunks, kNS>(
-                        P, tbound, tnode, tg, ws, o, d, pass == 0, q & kQMask, max_t, best, w_groups,
+                        P, tbound, tnode, tg, ws, o, d, pass == 0, q & kQMask, max_t, best, w_halves,
                         w_bounds, pt);
                 else
-                    scan_culled_lane<kStats>(P, tbound, tgroup, o, d, max_t, best, w_groups,
+                    scan_culled_lane<kStats>(P, tbound, tgroup, o, d, max_t, best, w_halves,
                                              w_bounds, lane_cnt, hit_groups);
                 if constexpr (kStats) pt.scan += ticks() - t0;
                 if constexpr (kStats) {  // CULL stats: debug[3] = sum of per-wave max lane need
@@ -1810,11 +1822,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 }
             } else {
                 scan_spheres<false>(P, lds_geom, n, o, d, max_t, best, hit_groups);
-                w_groups += (uint64_t)((n + 3) >> 2);
+                tally(w_halves, 2u * (uint32_t)((n + 3) >> 2));
             }
         } else {
             scan_spheres<kLds>(P, lds_geom, n, o, d, max_t, best, hit_groups);
-            w_groups += (uint64_t)((n + 3) >> 2);
+            tally(w_halves, 2u * (uint32_t)((n + 3) >> 2));
         }
         if constexpr (kStats) st_hitgroups += hit_groups;
 
@@ -1861,9 +1873,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) total += __shfl_xor(total, off);
     if (lane == 0 && total) atomicAdd(P.segments, total);
-    if (lane == 0 && P.work_done) {
-        atomicAdd(P.work_done + 0, (unsigned long long)(w_groups + w_pairs / 2u));
-        atomicAdd(P.work_done + 1, (unsigned long long)w_bounds);
+    if (P.work_done) {  // the tallies' wave sums (64-bit: a wave's total may pass 2^32)
+        unsigned long long wh = w_halves, wb = w_bounds;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            wh += __shfl_xor(wh, off);
+            wb += __shfl_xor(wb, off);
+        }
+        if (lane == 0) {
+            atomicAdd(P.work_done + 0, wh / 2u);
+            atomicAdd(P.work_done + 1, wb);
+        }
     }
     if constexpr (kStats) {
         if (lane == 0 && P.debug) {
