@@ -353,7 +353,7 @@ def main():
                          "traffic": prof.get("hbm_bytes_per_launch"),
                          "kernel": kernel, "kernel_ms": round(k_ms, 3),
                          "numerator": "issued fp32 work per launch: wave-level exact group "
-                                      "tests x 64 lanes x 4 x 23 + box tests x 64 x 26 "
+                                      "tests x 64 lanes x 4 x 23 + box tests x 64 x 27 "
                                       "(in-kernel counters; DESIGN.md 7)",
                          "issued_flops_per_launch": issued,
                          "segments_per_launch": int(seg),
