@@ -15,11 +15,14 @@ a.add_argument("code_object")
 a.add_argument("--chunk", type=int, default=0)
 a.add_argument("--worlds", default="1,8")
 a.add_argument("--ranks", type=int, default=2)
+a.add_argument("--tail", type=int, default=0)
+a.add_argument("--tail-chunk", type=int, default=0)
 args = a.parse_args()
 for world in [int(w) for w in args.worlds.split(",")]:
     for rank in range(min(world, args.ranks)):
         desc = vc.RenderDesc(width=1920, height=1080, samples_per_pixel=1024, max_depth=10,
                              device=0, rank=rank, world_size=world, accumulate_chunk=args.chunk,
+                             accumulate_tail=args.tail, accumulate_tail_chunk=args.tail_chunk,
                              code_object_path=args.code_object)
         with vc.Renderer(desc, "final") as r:
             r.draw_next_frame()
@@ -30,6 +33,7 @@ for world in [int(w) for w in args.worlds.split(",")]:
         t0 = d[9]
         ms = lambda t: round((t - t0) / 1e5, 3)  # 100 MHz ticks -> ms after the first start
         print(json.dumps({"world": world, "rank": rank, "chunk": st["accumulate_chunk"],
+                          "tail": [st["accumulate_tail"], st["accumulate_tail_chunk"]],
                           "kernel_ms": round(st["kernel_ms"], 3), "waves": waves,
                           "first_drained_ms": ms(d[10]),
                           "mean_drained_ms": ms(d[11] * 256 / waves),
