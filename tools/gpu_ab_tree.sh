@@ -19,19 +19,19 @@ run() {  # tag, env prefix, ab.py args
 C4="--spp 1024 --frames 2"
 S="--scene stress4096 --width 3840 --height 2160 --spp 32 --depth 50 --frames 2"
 for i in ${ROUNDS:-1 2}; do
-  run "prev c4" env VCRT_PKG_ROOT=ab_objs/prev python tools/ab.py default --rounds 1 $C4
+  run "prev c4" env VCRT_PKG_ROOT=${PREV:-ab_objs/prev} python tools/ab.py default --rounds 1 $C4
   run "new c4" python tools/ab.py default --rounds 1 $C4
   for o in $OBJS; do run "$o c4" python tools/ab.py $o --rounds 1 $C4; done
 done
 if [ -n "$STRESS" ]; then
-  run "prev stress" env VCRT_PKG_ROOT=ab_objs/prev python tools/ab.py default --rounds 1 $S
+  run "prev stress" env VCRT_PKG_ROOT=${PREV:-ab_objs/prev} python tools/ab.py default --rounds 1 $S
   run "new stress" python tools/ab.py default --rounds 1 $S
   for o in $OBJS; do run "$o stress" python tools/ab.py $o --rounds 1 $S; done
 fi
 if [ -n "$C2" ]; then
   C2A="--scene three --width 800 --height 450 --spp 64 --depth 8 --frames 20"
   for i in 1 2 3; do
-    run "prev c2" env VCRT_PKG_ROOT=ab_objs/prev python tools/ab.py default --rounds 1 $C2A
+    run "prev c2" env VCRT_PKG_ROOT=${PREV:-ab_objs/prev} python tools/ab.py default --rounds 1 $C2A
     run "new c2" python tools/ab.py default --rounds 1 $C2A
     for o in $OBJS; do run "$o c2" python tools/ab.py $o --rounds 1 $C2A; done
   done
