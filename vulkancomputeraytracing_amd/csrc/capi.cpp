@@ -544,9 +544,10 @@ KernelChoice select_kernel() {
     // copy for 16 waves); beyond that from global memory.
     const uint32_t tab_lds = static_cast<uint32_t>(16 * (g.ncgroups / 2 * 4 + g.ncgroups * 5));
     // flat: near/far boxes (80 B per pair, 336 B per node of 4 pairs: 16 B of bank padding),
-    // 80-B group records (the uint16 member indices inside)
-    const uint32_t tab_lds_flat =
-        static_cast<uint32_t>(16 * (g.ncgroups / 8 * 21 + g.ncgroups * 5));
+    // 80-B group records (the uint16 member indices inside), the chunks' node boxes (near/far,
+    // 336 B per chunk: the node level of a tracer.hip VCRT_LEVELS_NF build)
+    const uint32_t tab_lds_flat = static_cast<uint32_t>(
+        16 * (g.ncgroups / 8 * 21 + g.ncgroups * 5 + (g.ncgroups + 63) / 64 * 21));
     const bool lane_lds = tab_lds <= g.max_lds && g.cull_lane_tables != 2;
     const bool lane_wide = lane_lds && tab_lds > 32768u;
     int variant = g.desc.kernel_variant;

@@ -225,6 +225,9 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
 //      rules a box out when its whole stretch of the line lies behind -tau as well.
 //      (tau = sqrt(3.2e-7 Q / a), 7% above 5.02u Q / a for the roundings of Q, 1/a and sqrt.)
 // Waves holding a ray outside the guarded range scan the original table in reference order.
+#ifndef VCRT_LEVELS_NF
+#define VCRT_LEVELS_NF 1  // the LDS-table kernel's node level by near/far planes from LDS (0: scalar min/max)
+#endif
 #ifndef VCRT_BOX_CLIP
 #define VCRT_BOX_CLIP 1  // (4): 0 = the line test alone (A/B builds)
 #endif
@@ -1075,6 +1078,15 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             // chunk, per-lane bits -> node entries
             const int nn = min(8, (ncg - base) >> 3);
             uint32_t out = 0;
+#if VCRT_LEVELS_NF
+            {  // near/far planes from the LDS copy of the chunk's node boxes, by the ray's signs
+                const NearFarAddr na = near_far_addr(tnode + kNS * ((uint32_t)base >> 6),
+                                                     br.ix.x, br.iy.x, br.iz.x);
+#pragma unroll
+                for (int k = 3; k >= 0; k--) out = push_bound_pair_nf(out, br, na, 80 * k);
+                out &= (1u << nn) - 1u;
+            }
+#else
             cfloat4* nb = node + 4 * (base >> 4);
             BoundPair cur = load_bound_pair(nb + 4 * ((nn - 2) >> 1));
             for (int j = nn - 2; j >= 0; j -= 2) {
@@ -1082,6 +1094,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                 out = push_bound_pair(out, br, cur.b0, cur.b1, cur.b2, cur.b3);
                 cur = nxt;
             }
+#endif
             n_bounds += (uint32_t)nn;
             uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
             if constexpr (kStats) {
@@ -1334,6 +1347,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     }
     if constexpr (kCull == 4) {  // LDS: near/far boxes, 80-B group records with uint16 indices
         const int nb = (P.ncgroups >> 3) * kNS, ng = P.ncgroups * 5;
+#if VCRT_LEVELS_NF
+        {  // and the chunks' node boxes (near/far, padded records) after the group records
+            const int nn = ((P.ncgroups + 63) >> 6) * kNS;
+            for (int i = threadIdx.x; i < nn; i += blockDim.x)
+                if (i % kNS != 20u) lds_geom[nb + ng + i] = tnode[i - i / kNS];
+        }
+#endif
         for (int i = threadIdx.x; i < nb; i += blockDim.x)
             if (i % kNS != 20u) lds_geom[i] = tbound[i - i / kNS];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) {
@@ -1350,7 +1370,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         __syncthreads();
         tbound = lds_geom;
         tg.geom = lds_geom + nb;
+#if VCRT_LEVELS_NF
+        tnode = lds_geom + nb + ng;
+        ws = reinterpret_cast<WS*>(lds_geom + nb + ng + ((P.ncgroups + 63) >> 6) * kNS) +
+             (threadIdx.x >> 6);
+#else
         ws = reinterpret_cast<WS*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
+#endif
         static_assert(kNS == 21u && sizeof(WS) == kWaveScratchBytes8,
                       "host LDS size (capi.cpp select_kernel)");
     }
