@@ -208,7 +208,7 @@ def test_per_lane_culled_scan_table_placement(oracle, monkeypatch, tables, scene
     assert st["segments"] == segs
     if tables == "global":
         assert st["tables_in_lds"] == 0
-        assert st["lds_bytes"] == 4 * 6912 and st["block_threads"] == 256
+        assert st["lds_bytes"] == 4 * 6920 and st["block_threads"] == 256
     elif scene == "final":
         assert st["tables_in_lds"] == 1 and st["block_threads"] == 256
     else:
@@ -252,7 +252,7 @@ def test_flat_scan_boxes_in_lds(oracle, monkeypatch, scene, w, h, spp, depth, ch
         assert st["kernel"] == "vcrt_trace_cull_flat_global"
     else:
         assert st["kernel"] == "vcrt_trace_cull_flat_boxes"
-        assert st["block_threads"] == 1024 and st["lds_bytes"] > 16 * 4352
+        assert st["block_threads"] == 1024 and st["lds_bytes"] > 16 * 4360
 
 
 def culling_torture_scene():

@@ -57,6 +57,13 @@ __device__ __forceinline__ void tally(uint32_t& t, uint32_t x) {
     t += (threadIdx.x & 63u) == first ? x : 0u;
 }
 
+// tally into a per-wave LDS counter (the flat scans' WaveScratch::work): one LDS add from the
+// first active lane, nothing held in VGPRs across the loop
+__device__ __forceinline__ void tally_lds(uint32_t* slot, uint32_t x) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+    if ((threadIdx.x & 63u) == first) atomicAdd(slot, x);
+}
+
 typedef __attribute__((address_space(4))) const float4 cfloat4;
 
 // One group = four spheres in pair-SoA form: q[0] = (cx0,cx1,cy0,cy1), q[1] = (cz0,cz1,r0²,r1²),
@@ -707,12 +714,13 @@ struct WaveScratch {
     using entry_t = typename FlatFmt<kFmt>::entry_t;
     static constexpr bool kHasChunks = kChunks;
     unsigned long long key[64];  // per owner lane: (bits(t) << 32) | sphere index
+    uint32_t work[2];            // issued-work tallies of the flat scan: half-groups, box tests
     typename FlatFmt<kFmt>::cand_t cand[kCandCap];  // group entry << 2 | member
     entry_t group[kGroupCap];    // owner << kShift | group
     entry_t node[kNodeCap];      // owner << kShift | node
     entry_t chunk[kChunks ? kChunkCap : 0];  // owner << kShift | chunk (64 groups)
 };
-static_assert(sizeof(WaveScratch<0, false>) == kWaveScratchBytes8, "host LDS size");
+static_assert(sizeof(WaveScratch<0, false>) == kWaveScratchBytes8, "host LDS size");  // 3464
 static_assert(sizeof(WaveScratch<1>) == kWaveScratchBytes, "host LDS size");
 static_assert(sizeof(WaveScratch<2>) == kWaveScratchBytesWide, "host LDS size");
 
@@ -1124,8 +1132,10 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     const unsigned long long k = ws->key[lane];
     max_t = __uint_as_float((uint32_t)(k >> 32));
     best = (int)(uint32_t)k;
-    tally(bounds_tested, __builtin_amdgcn_readfirstlane(n_bounds));
-    tally(groups_tested, 2u * __builtin_amdgcn_readfirstlane(n_groups));  // half-groups
+    (void)groups_tested;
+    (void)bounds_tested;
+    tally_lds(&ws->work[1], __builtin_amdgcn_readfirstlane(n_bounds));
+    tally_lds(&ws->work[0], 2u * __builtin_amdgcn_readfirstlane(n_groups));  // half-groups
 }
 
 template <bool kStats>
@@ -1443,6 +1453,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     uint32_t ring_pos = 0u, blk_ps0 = 0u, blk_ring = 0u;
     if (ring) {
         for (uint32_t i = lane; i < P.ring_n; i += 64u) ring[i].q = ~0u;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (kFlat) {
+        if (lane < 2u) ws->work[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
     }
 
@@ -1793,7 +1807,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 }
                 // issued work: the big list and the loop's passes (a pair test is half a group
                 // test), per wave
-                tally(w_halves, 2u * (uint32_t)P.nbig + wave_max_small<3>(iters));
+                tally_lds(&ws->work[0], 2u * (uint32_t)P.nbig + wave_max_small<3>(iters));
             }
             // One shading for the camera rays just traced and the main-scan hits of the last
             // iteration: the hit branches run once per iteration for both (a lane has at most
@@ -1848,7 +1862,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 }
             } else {
                 scan_spheres<false>(P, lds_geom, n, o, d, max_t, best, hit_groups);
-                tally(w_halves, 2u * (uint32_t)((n + 3) >> 2));
+                if constexpr (kFlat)
+                    tally_lds(&ws->work[0], 2u * (uint32_t)((n + 3) >> 2));
+                else
+                    tally(w_halves, 2u * (uint32_t)((n + 3) >> 2));
             }
         } else {
             scan_spheres<kLds>(P, lds_geom, n, o, d, max_t, best, hit_groups);
@@ -1905,6 +1922,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         for (int off = 32; off > 0; off >>= 1) {
             wh += __shfl_xor(wh, off);
             wb += __shfl_xor(wb, off);
+        }
+        if constexpr (kFlat) {  // and the flat scan's per-wave LDS tallies
+            __builtin_amdgcn_wave_barrier();
+            wh += ws->work[0];
+            wb += ws->work[1];
         }
         if (lane == 0) {
             atomicAdd(P.work_done + 0, wh / 2u);

@@ -92,9 +92,9 @@ constexpr uint32_t kRingQBits = 26;
 
 constexpr int32_t kFlatMaxGroups = 1024;   // CULL_FLAT 16-bit entries: 10-bit group / node fields
 constexpr int32_t kFlatMaxGroups8 = 256;   // the LDS-table kernel: 8-bit fields, 16-bit candidates
-constexpr uint32_t kWaveScratchBytes = 4352;   // CULL_FLAT per-wave LDS stacks, 16-bit entries
-constexpr uint32_t kWaveScratchBytes8 = 3456;  // 16-bit candidates, no chunk stack (LDS tables)
-constexpr uint32_t kWaveScratchBytesWide = 6912;  // the same with 32-bit entries (global tables)
+constexpr uint32_t kWaveScratchBytes = 4360;   // CULL_FLAT per-wave LDS stacks, 16-bit entries
+constexpr uint32_t kWaveScratchBytes8 = 3464;  // 16-bit candidates, no chunk stack (LDS tables)
+constexpr uint32_t kWaveScratchBytesWide = 6920;  // the same with 32-bit entries (global tables)
 constexpr uint32_t kFlagReverseOrder = 1u;  // hand out work items last-to-first
 constexpr uint32_t kFlagSceneBounded = 2u;  // every |center|, radius <= 2^30 (host-checked)
 constexpr uint32_t kFlagChunkMinor = 8u;  // a block's 64 items run chunk-minor: all chunks of
