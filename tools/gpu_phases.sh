@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-VCRT_DEBUG_STATS=1 timeout -k 10 200 python tools/render_once.py --spp 64 --variant ${PV:-5} > gpurun_out/phases.json || exit 1
+VCRT_DEBUG_STATS=1 timeout -k 10 200 python tools/render_once.py ${RO:---spp 64} --variant ${PV:-5} > gpurun_out/phases.json || exit 1
 python - <<'PY'
 import json
 st = json.load(open("gpurun_out/phases.json"))
