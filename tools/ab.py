@@ -51,7 +51,8 @@ def main():
                                      "msamples_per_s": st["samples"] / (ms * 1e3),
                                      "segments": st["segments"],
                                      "group_tests": st["group_tests"],
-                                     "bound_tests": st["bound_tests"]}
+                                     "bound_tests": st["bound_tests"],
+                                     "ring_entries": st["ring_entries"]}
                 if rnd == 0:
                     digest[obj] = hashlib.sha256(r.read_framebuffer().tobytes()).hexdigest()[:16]
             for kv in filter(None, env.split(",")):
