@@ -6,7 +6,9 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# VCRT_PKG_ROOT: the package (and its libvcrt.so) of another tree (tools/mkab_tree.sh), for A/B
+sys.path.insert(0, os.environ.get("VCRT_PKG_ROOT",
+                                  os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import vulkancomputeraytracing_amd as vc  # noqa: E402
 
 p = argparse.ArgumentParser()
