@@ -24,9 +24,11 @@ for i in ${ROUNDS:-1 2}; do
   for o in $OBJS; do run "$o c4" python tools/ab.py $o --rounds 1 $C4; done
 done
 if [ -n "$STRESS" ]; then
-  run "prev stress" env VCRT_PKG_ROOT=${PREV:-ab_objs/prev} python tools/ab.py default --rounds 1 $S
-  run "new stress" python tools/ab.py default --rounds 1 $S
-  for o in $OBJS; do run "$o stress" python tools/ab.py $o --rounds 1 $S; done
+  for i in ${STRESS_ROUNDS:-1}; do
+    run "prev stress" env VCRT_PKG_ROOT=${PREV:-ab_objs/prev} python tools/ab.py default --rounds 1 $S
+    run "new stress" python tools/ab.py default --rounds 1 $S
+    for o in $OBJS; do run "$o stress" python tools/ab.py $o --rounds 1 $S; done
+  done
 fi
 if [ -n "$C2" ]; then
   C2A="--scene three --width 800 --height 450 --spp 64 --depth 8 --frames 20"
