@@ -228,16 +228,32 @@ def main():
     if world > 1 and backend == "nccl":
         ids = [vc.renderer.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
-        r.comm_init(ids[0])
-        gather = "rccl in libvcrt (vcrt_draw_next_frame: grouped send/recv to rank 0)"
-    elif world > 1:
+        ok = 1
+        try:
+            r.comm_init(ids[0])
+        except vc.VcrtError as e:  # vcrt_comm_init released whatever it had set up
+            log(f"[rank {rank}] vcrt_comm_init failed: {e}")
+            ok = 0
+        # every rank learns whether all joined; if one did not, all gather through gloo so the
+        # job still measures the frame (the JSON's config.gather names the path that ran)
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if flag.item() == 1:
+            gather = "rccl in libvcrt (vcrt_draw_next_frame: grouped send/recv to rank 0)"
+        else:
+            log(f"[rank {rank}] RCCL gather unavailable on some rank: gloo gather instead")
+            r.close()  # a fresh renderer without a communicator (vcrt_end drops it if held)
+            r = vc.Renderer(desc, args.scene)
+            backend = "gloo-fallback"
+    if world > 1 and backend != "nccl":
         dev = torch.device("cuda", device)
         tiles_pad = D.tiles_per_rank(args.width, args.height, world)
         local = torch.zeros((tiles_pad * 64, 4), dtype=torch.float32, device=dev)
         r.set_framebuffer_device(local.data_ptr(), local.numel() * 4)
         if rank == 0:
             frame = torch.empty((args.height, args.width, 4), dtype=torch.float32, device=dev)
-        gather = "gloo rehearsal (torch.distributed.gather of host copies)"
+        gather = ("gloo fallback after vcrt_comm_init failed" if backend == "gloo-fallback" else
+                  "gloo rehearsal") + " (torch.distributed.gather of host copies)"
 
     def step():
         r.draw_next_frame()  # N > 1 (RCCL): returns on rank 0 with the gathered frame

@@ -581,6 +581,34 @@ def test_bench_multirank_gather_bitwise():
     assert res["validated"]["bitwise_vs_oracle"] is True
 
 
+def test_bench_rccl_init_failure_falls_back_to_gloo():
+    """bench.py's default N-rank path (RCCL inside libvcrt) when vcrt_comm_init fails on a rank:
+    two ranks on one GPU (RCCL refuses a duplicate device). Every rank sees the failure through
+    the all-reduced flag, opens a fresh renderer and gathers through gloo; the job completes,
+    names the path in config.gather, and the frame is bit-identical to a 1-GPU render."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k != "VCRT_DIST_BACKEND"}
+    env["VCRT_COMM_TIMEOUT_MS"] = "20000"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--width", "160", "--height", "96",
+           "--spp", "8", "--depth", "10", "--scene", "final", "--no-cpu-baseline", "--validate"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2
+    assert res["config"]["gather"].startswith("gloo fallback"), res["config"]["gather"]
+    assert res["validated"]["bitwise_vs_1gpu"] is True
+
+
 def test_rccl_comm_inside_libvcrt_world1(oracle):
     """vcrt_comm_init (RCCL linked into libvcrt.so) on a one-rank communicator: the
     communicator comes up on the GPU, frames draw through the gather-aware path, the frame is
