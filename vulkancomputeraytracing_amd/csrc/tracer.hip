@@ -1905,6 +1905,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         atomicMin(P.debug + 9, t_start_rt);
         atomicMin(P.debug + 10, t_drained_rt);
         atomicAdd(P.debug + 11, t_drained_rt >> 8);
+        // wave lifetimes in 0.1 ms buckets (debug 12..27, the last open-ended) and how long
+        // the wave ran on after it saw the queue drained (28..31: < 0.1, < 0.3, < 0.6 ms, more)
+        const unsigned long long life = (t - t_start_rt) / 10000ull;
+        atomicAdd(P.debug + 12 + (life < 15ull ? life : 15ull), 1ull);
+        const unsigned long long after = t_drained_rt == ~0ull ? 0ull : (t - t_drained_rt) / 10000ull;
+        atomicAdd(P.debug + (after < 1ull ? 28 : after < 3ull ? 29 : after < 6ull ? 30 : 31), 1ull);
     }
 #endif
     if (ring) {  // the wave's remaining partial sums (every lane of the wave is here)
