@@ -34,7 +34,8 @@ namespace {
 
 using vcrt::to_vk;
 
-constexpr size_t kCounterBytes = 256;  // work (u32), segments (u64), work_done[2] (u64), padded
+// segments (u64 at 8), work_done[2] (u64 at 16), then the eight work-queue counters from 256
+constexpr size_t kCounterBytes = 256 + 8 * 4 * vcrt::kQueueStride;
 constexpr int32_t kDefaultChunk = 64;        // samples per work item (upper end)
 
 struct RendererState {
@@ -992,7 +993,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.jitter = g.d_jitter;
         p.out = g.d_fb;
         p.accum = g.d_accum;
-        p.work = static_cast<uint32_t*>(g.d_counters);
+        p.work = reinterpret_cast<uint32_t*>(static_cast<char*>(g.d_counters) + 256);
         p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
         p.debug = static_cast<unsigned long long*>(g.d_debug);
         p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);

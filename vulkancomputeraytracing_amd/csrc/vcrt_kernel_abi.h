@@ -29,7 +29,7 @@ struct TraceParams {
     float4* out;           // rank-local framebuffer, rgba32f (layout above)
     double* accum;         // [local_tiles * 64][4] exact sums of the quantized chunk sums (r, g,
                            //   b, unused), vcrt_math.h "Accumulation"; unused with kFlagDirect
-    uint32_t* work;        // work-item counter, zeroed before every launch
+    uint32_t* work;        // eight work-queue counters kQueueStride apart, zeroed every launch
     unsigned long long* segments;  // ray segments traced, zeroed before every launch
     unsigned long long* debug;     // diagnostics counters (stats kernels only), may be null
     unsigned long long* work_done;  // [2]: sphere groups tested, group bounds tested
@@ -87,6 +87,7 @@ struct TraceParams {
     uint32_t ring_off, ring_n;
 };
 
+constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
 constexpr uint32_t kRingMaxEntries = 63;  // entry + 1 in the top 6 bits of a lane's pixel index
 constexpr uint32_t kRingQBits = 26;
 
