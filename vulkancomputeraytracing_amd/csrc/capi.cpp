@@ -34,8 +34,8 @@ namespace {
 
 using vcrt::to_vk;
 
-// segments (u64 at 8), work_done[2] (u64 at 16), then the eight work-queue counters from 256
-constexpr size_t kCounterBytes = 256 + 8 * 4 * vcrt::kQueueStride;
+// segments (u64 at 8), work_done[2] (u64 at 16), then the work-queue counters from 256
+constexpr size_t kCounterBytes = 256 + vcrt::kMaxQueues * 4 * vcrt::kQueueStride;
 constexpr int32_t kDefaultChunk = 64;        // samples per work item (upper end)
 
 struct RendererState {

@@ -1442,7 +1442,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     // the wave's current block of items (wave-uniform); 64 = exhausted, fetch a new one
     const uint32_t total_blocks = P.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
-    uint32_t q_x = blockIdx.x & 7u, q_drained = 0u;  // the wave's work queue; queues found empty
+    uint32_t q_x = blockIdx.x & (kQueues - 1u), q_drained = 0u;  // the wave's queue; found empty
     uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
     bool blk_tail = false;
     // the wave's accumulation ring (see RingEntry): next entry to hand out; the current block's
@@ -1625,21 +1625,22 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         while (need_mask) {
             if (blk_next >= 64u) {
                 if constexpr (kStats && kCull == 0) ++st_fetch;
-                // eight queues, one per XCD (workgroups are dispatched to the XCDs round
-                // robin): queue x hands out blocks 8 k + x, on its own counter; a wave whose
-                // queue is drained moves on to the next one, and is done when all eight are
+                // kQueues queues, each on workgroups of one XCD (workgroups are dispatched to
+                // the XCDs round robin): queue x hands out blocks kQueues k + x on its own
+                // counter; a wave whose queue is drained moves on to the next one, and is done
+                // when it has found every queue drained
                 uint32_t b = ~0u;
-                while (q_drained < 8u) {
+                while (q_drained < kQueues) {
                     const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
                     uint32_t k = 0;
                     if ((int)lane == leader) k = atomicAdd(P.work + kQueueStride * q_x, 1u);
                     k = __builtin_amdgcn_readfirstlane(__shfl(k, leader));
-                    if (k < (total_blocks + 7u - q_x) >> 3) {
-                        b = 8u * k + q_x;
+                    if (k < (total_blocks + kQueues - 1u - q_x) / kQueues) {
+                        b = kQueues * k + q_x;
                         break;
                     }
                     ++q_drained;
-                    q_x = (q_x + 1u) & 7u;
+                    q_x = (q_x + 1u) & (kQueues - 1u);
                 }
                 if (b == ~0u) {  // queues drained: lanes still wanting work are done
 #ifdef VCRT_WAVE_END_TIMES

@@ -88,6 +88,13 @@ struct TraceParams {
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
+#ifndef VCRT_QUEUES
+#define VCRT_QUEUES 32
+#endif
+// work queues (a power of two): queue x serves workgroups x, x + kQueues, ..., which all sit
+// on XCD x % 8; 32 (four per XCD) measured at or above 8 and 16 (profiles/r03_ab_log.md)
+constexpr uint32_t kQueues = VCRT_QUEUES;
+constexpr uint32_t kMaxQueues = 32;        // counters the host allocates and zeroes
 constexpr uint32_t kRingMaxEntries = 63;  // entry + 1 in the top 6 bits of a lane's pixel index
 constexpr uint32_t kRingQBits = 26;
 
