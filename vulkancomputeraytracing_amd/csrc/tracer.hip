@@ -1443,6 +1443,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     const uint32_t total_blocks = P.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
     uint32_t q_x = blockIdx.x & (kQueues - 1u), q_drained = 0u;  // the wave's queue; found empty
+#ifdef VCRT_PAIR_FETCH
+    uint32_t q_pend = ~0u;
+    bool q_pair = true;
+#endif
     uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
     bool blk_tail = false;
     // the wave's accumulation ring (see RingEntry): next entry to hand out; the current block's
@@ -1630,17 +1634,36 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // counter; a wave whose queue is drained moves on to the next one, and is done
                 // when it has found every queue drained
                 uint32_t b = ~0u;
-                while (q_drained < kQueues) {
+#ifdef VCRT_PAIR_FETCH  // experiment: two blocks per fetch while the queue is < 3/4 handed out
+                if (q_pend != ~0u) {
+                    b = q_pend;
+                    q_pend = ~0u;
+                }
+#endif
+                while (b == ~0u && q_drained < kQueues) {
                     const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+                    const uint32_t nq = (total_blocks + kQueues - 1u - q_x) / kQueues;
                     uint32_t k = 0;
-                    if ((int)lane == leader) k = atomicAdd(P.work + kQueueStride * q_x, 1u);
+#ifdef VCRT_PAIR_FETCH
+                    const uint32_t amt = q_pair ? 2u : 1u;
+#else
+                    const uint32_t amt = 1u;
+#endif
+                    if ((int)lane == leader) k = atomicAdd(P.work + kQueueStride * q_x, amt);
                     k = __builtin_amdgcn_readfirstlane(__shfl(k, leader));
-                    if (k < (total_blocks + kQueues - 1u - q_x) / kQueues) {
+                    if (k < nq) {
                         b = kQueues * k + q_x;
+#ifdef VCRT_PAIR_FETCH
+                        if (amt == 2u && k + 1u < nq) q_pend = b + kQueues;
+                        q_pair = 4u * k < 3u * nq;
+#endif
                         break;
                     }
                     ++q_drained;
                     q_x = (q_x + 1u) & (kQueues - 1u);
+#ifdef VCRT_PAIR_FETCH
+                    q_pair = false;
+#endif
                 }
                 if (b == ~0u) {  // queues drained: lanes still wanting work are done
 #ifdef VCRT_WAVE_END_TIMES
