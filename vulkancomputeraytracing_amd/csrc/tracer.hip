@@ -1443,6 +1443,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     const uint32_t total_blocks = P.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
     uint32_t q_x = blockIdx.x & (kQueues - 1u), q_drained = 0u;  // the wave's queue; found empty
+#ifdef VCRT_STATIC_FIRST  // experiment: each wave's first block of its queue without an atomic
+    // (the queue's k-th wave takes its k-th block; the counter then counts past those)
+    const uint32_t q_wpg = blockDim.x >> 6;
+    uint32_t q_first = (blockIdx.x / kQueues) * q_wpg + (threadIdx.x >> 6);
+#endif
 #ifdef VCRT_PAIR_FETCH
     uint32_t q_pend = ~0u;
     bool q_pair = true;
@@ -1634,6 +1639,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // counter; a wave whose queue is drained moves on to the next one, and is done
                 // when it has found every queue drained
                 uint32_t b = ~0u;
+#ifdef VCRT_STATIC_FIRST
+                if (q_first != ~0u) {
+                    if (q_first < (total_blocks + kQueues - 1u - q_x) / kQueues)
+                        b = kQueues * q_first + q_x;
+                    q_first = ~0u;
+                }
+#endif
 #ifdef VCRT_PAIR_FETCH  // experiment: two blocks per fetch while the queue is < 3/4 handed out
                 if (q_pend != ~0u) {
                     b = q_pend;
@@ -1651,6 +1663,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 #endif
                     if ((int)lane == leader) k = atomicAdd(P.work + kQueueStride * q_x, amt);
                     k = __builtin_amdgcn_readfirstlane(__shfl(k, leader));
+#ifdef VCRT_STATIC_FIRST
+                    k += ((gridDim.x + kQueues - 1u - q_x) / kQueues) * q_wpg;  // q_x's static
+#endif
                     if (k < nq) {
                         b = kQueues * k + q_x;
 #ifdef VCRT_PAIR_FETCH
