@@ -65,7 +65,9 @@ def parse():
     p.add_argument("--validate", action="store_true",
                    help="after the timed steps, rank 0 checks its frame: bit for bit against the "
                         "CPU oracle on a few rows at full spp, and (N > 1) against a 1-GPU "
-                        "render of the whole frame")
+                        "render of the whole frame. Always on when N > 1 (the multi-GPU line "
+                        "proves its own gather); --no-validate turns it off")
+    p.add_argument("--no-validate", action="store_true")
     p.add_argument("--validate-rows", type=int, default=2)
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU work for the cpu_baseline sample")
@@ -166,7 +168,8 @@ def cpu_baseline(args):
 
 def validate(args, got, st, device, world):
     """Rank 0's frame against the CPU oracle on a few full-width rows at full spp and depth
-    (bit for bit, same accumulation chunk), and for N > 1 against a 1-GPU render."""
+    (bit for bit, same accumulation quantum), and for N > 1 against a default 1-GPU render of
+    the whole frame: the image depends on the quantum alone, which does not depend on N."""
     import numpy as np
     from tests import oracle_py
     import vulkancomputeraytracing_amd as vc
@@ -181,15 +184,14 @@ def validate(args, got, st, device, world):
     out["bitwise_vs_oracle"] = bool(np.array_equal(got[rows].view(np.uint32),
                                                    want.view(np.uint32)))
     if world > 1:
-        # the same chunk partition as the ranks used: then the frames are equal bit for bit
+        # the default 1-GPU frame (its own work items): equal bit for bit when the gather is right
         ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
-                                 max_depth=args.depth, device=device, kernel_variant=args.variant,
-                                 accumulate_chunk=st["accumulate_chunk"],
-                                 accumulate_tail=st["accumulate_tail"] or -1,
-                                 accumulate_tail_chunk=st["accumulate_tail_chunk"])
+                                 max_depth=args.depth, device=device, kernel_variant=args.variant)
         with vc.Renderer(ref_desc, args.scene) as ref:
             ref.draw_next_frame()
             one = ref.read_framebuffer()
+            q1 = ref.stats()["accumulate_quantum"]
+        out["quantum"] = [st["accumulate_quantum"], q1]
         out["bitwise_vs_1gpu"] = bool(np.array_equal(got.view(np.uint32), one.view(np.uint32)))
     log(f"validate: {out}")
     return out
@@ -291,8 +293,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = r.stats()
+    # per-rank kernel times (the balance of the shards) for the JSON line
+    k_mean = sum(kernel_ms) / len(kernel_ms)
+    rank_ms = [k_mean]
+    if world > 1:
+        rank_ms = [None] * world
+        dist.all_gather_object(rank_ms, k_mean)
+    do_validate = (args.validate or world > 1) and not args.no_validate
     got = None
-    if args.validate and rank == 0:  # a host copy, before the renderer closes
+    if do_validate and rank == 0:  # a host copy, before the renderer closes
         got = frame.cpu().numpy() if frame is not None else r.read_framebuffer()
     # close before validate(): libvcrt keeps one renderer per process, and validate() opens
     # its own (a second vcrt_begin would end this one, communicator included)
@@ -352,6 +361,7 @@ def main():
                        "height": args.height, "spp": args.spp, "max_depth": args.depth,
                        "parallelism": f"tiles8x8-diagonal-x{world}",
                        "gather": gather,
+                       "accumulate_quantum": st["accumulate_quantum"],
                        "accumulate_chunk": st["accumulate_chunk"],
                        "accumulate_tail": [st["accumulate_tail"], st["accumulate_tail_chunk"]],
                        "kernel_variant": st["kernel_variant"],
@@ -381,6 +391,8 @@ def main():
                          "effective_clock_ghz": prof.get("effective_clock_ghz"),
                          "profile": prof.get("source")},
             "gather_ms": round(sum(gather_ms) / len(gather_ms), 3),
+            "per_rank_kernel_ms": {"min": round(min(rank_ms), 3), "max": round(max(rank_ms), 3),
+                                   "ranks": [round(v, 3) for v in rank_ms]},
         }
         if validated is not None:
             out["validated"] = validated

@@ -93,16 +93,9 @@ typedef struct vcrt_render_desc {
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
     int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 16 while the
-                                 largest rank's share has < 2^24 - 2^21 items, at least
-                                 spp / 512:
-                                 vcrt_work_chunk). A pixel's samples are summed in fp32 in order
-                                 within a chunk; one chunk (>= samples_per_pixel) is divided in
-                                 fp32, the reference's sequential sum (shader.comp:46-56)
-                                 exactly; several chunk sums are quantized to 2^-32 and added
-                                 exactly, so the image depends on the chunk partition (this
-                                 and the tail below) only, not on the schedule: a sharded frame
-                                 equals a one-GPU render with the same partition. At most 512
-                                 chunks per pixel (tail and progressive frames included). */
+                                 largest rank's share has < 2^24 - 2^21 items: vcrt_work_chunk),
+                                 rounded up to a multiple of the quantum below. A scheduling
+                                 choice only: it does not change the image. */
     int32_t progressive; /* 0: every DrawNextFrame re-renders samples 0..spp-1 (the reference,
                             Linux.cpp:362-366). 1: frame f renders samples f*spp..(f+1)*spp-1 and
                             the framebuffer holds the average of all frames so far (the same
@@ -115,7 +108,21 @@ typedef struct vcrt_render_desc {
                                      running when the queue drains are short. 0 = the rule
                                      (vcrt_work_tail), -1 = none. Part of the chunk partition: the
                                      image depends on it as on accumulate_chunk. */
-    int32_t accumulate_tail_chunk; /* samples per tail item; 0 = the rule */
+    int32_t accumulate_tail_chunk; /* samples per tail item; 0 = the rule. Tail and tail items
+                                      are rounded to multiples of the quantum. */
+    int32_t accumulate_quantum; /* the accumulation quantum G (a power of two; 0 = the rule,
+                                   vcrt_work_quantum: 16, doubled while a pixel would take more
+                                   than 512 quanta). A pixel's samples are summed in fp32 in sample
+                                   order within each quantum of G consecutive samples (restarting
+                                   at every progressive frame); when one quantum covers the pixel
+                                   (G >= samples_per_pixel, not progressive) the sum is divided in
+                                   fp32, the reference's sequential sum (shader.comp:46-56)
+                                   exactly; otherwise every quantum sum is quantized to 2^-32 and
+                                   added exactly. So the image depends on G only -- not on the
+                                   work items, the schedule or the number of GPUs: a sharded frame
+                                   equals a one-GPU render bit for bit. Work items hold whole
+                                   quanta. At most 512 quanta per pixel (progressive frames
+                                   included). */
 } vcrt_render_desc;
 
 typedef struct vcrt_stats {
@@ -131,7 +138,7 @@ typedef struct vcrt_stats {
     int32_t local_tiles;   /* 8x8 tiles this rank renders */
     int32_t nspheres;
     uint32_t lds_bytes;    /* dynamic LDS of the tracer's tables and stacks (without the ring) */
-    int32_t accumulate_chunk; /* samples per work item in effect */
+    int32_t accumulate_chunk; /* samples per work item in effect (head) */
     int32_t tables_in_lds;    /* 1 when the culled scan reads its tables from LDS, 2 when only
                                  its boxes (vcrt_trace_cull_flat_boxes) */
     uint64_t accumulated_spp; /* samples per pixel in the framebuffer (progressive: all frames) */
@@ -152,7 +159,7 @@ typedef struct vcrt_stats {
     int32_t accumulate_tail_chunk; /* samples per tail item in effect */
     int32_t ring_entries;          /* LDS accumulation ring entries per wave (0: none; the chunk
                                       sums go to global memory directly) */
-    int32_t reserved0;
+    int32_t accumulate_quantum;    /* the accumulation quantum G in effect */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
@@ -160,16 +167,18 @@ typedef struct vcrt_stats {
 vcrt_result vcrt_default_desc(vcrt_render_desc* desc);
 
 vcrt_result vcrt_begin(const vcrt_render_desc* desc);
-/* Samples per work item (the accumulation chunk) that vcrt_begin(desc) uses; host only, no
- * GPU. Negative VkResult for an invalid desc. */
+/* The accumulation quantum G that vcrt_begin(desc) uses (the image depends on it alone); host
+ * only, no GPU. Negative VkResult for an invalid desc. */
+int32_t vcrt_work_quantum(const vcrt_render_desc* desc);
+/* Samples per work item of the head that vcrt_begin(desc) uses (a multiple of the quantum);
+ * host only, no GPU. Negative VkResult for an invalid desc. */
 int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
 /* Tail samples per pixel that vcrt_begin(desc) uses (0: none) and, in *tail_chunk, the samples
  * per tail item; host only. The rule: about six head items per lane of the persistent grid,
  * T = 6 * chunk * 327680 / (64 * the largest rank's tiles) rounded to a power of two, in items
- * of max(4, chunk / 8) samples; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel.
- * Head and tail together take at most 512 chunks per pixel: a rule-made tail item grows until
- * the tail fits beside the head (or the tail is dropped when the head leaves no room).
- * Negative VkResult for an invalid desc. */
+ * of one quantum; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel. The head
+ * ends on a quantum boundary (T is adjusted) and tail items are whole quanta. Negative VkResult
+ * for an invalid desc. */
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
  * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final

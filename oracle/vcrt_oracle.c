@@ -141,10 +141,34 @@ float oracle_sin(float xf) {
     return (float)s;
 }
 
+/* ------------------------------------------------------------------------------------ */
+/* The reference's literals, named once (pinned against the reference files by            */
+/* tests/golden/reference_constants.json; oracle_reference_constants exports them).        */
+#define ORACLE_RAND_DOT_X 12.9898f     /* functions.glsl:11 */
+#define ORACLE_RAND_DOT_Y 78.233f      /* functions.glsl:11 */
+#define ORACLE_RAND_SCALE 43758.5453f  /* functions.glsl:11 */
+#define ORACLE_MIN_T 0.001f            /* functions.glsl:76 */
+#define ORACLE_INFINITY 1e5f           /* globals.glsl:26, functions.glsl:75 */
+#define ORACLE_SKY_HALF 0.5f           /* functions.glsl:87 */
+#define ORACLE_SKY_ONE 1.0f            /* functions.glsl:87 */
+#define ORACLE_SKY_BOTTOM 1.0f         /* functions.glsl:88 vec3(1) */
+#define ORACLE_SKY_TOP_R 0.5f          /* functions.glsl:88 vec3(.5,.7,1) */
+#define ORACLE_SKY_TOP_G 0.7f
+#define ORACLE_SKY_TOP_B 1.0f
+#define ORACLE_JITTER_OFFSET (-0.5f)   /* shader.comp:48 */
+
+void oracle_reference_constants(float out[ORACLE_NCONSTANTS]) {
+    const float c[ORACLE_NCONSTANTS] = {ORACLE_RAND_DOT_X, ORACLE_RAND_DOT_Y, ORACLE_RAND_SCALE,
+                                        ORACLE_MIN_T,      ORACLE_INFINITY,   ORACLE_SKY_HALF,
+                                        ORACLE_SKY_ONE,    ORACLE_SKY_BOTTOM, ORACLE_SKY_TOP_R,
+                                        ORACLE_SKY_TOP_G,  ORACLE_SKY_TOP_B,  ORACLE_JITTER_OFFSET};
+    memcpy(out, c, sizeof(c));
+}
+
 /* functions.glsl:10-12  rand(co) = fract(sin(dot(co, vec2(12.9898,78.233))) * 43758.5453) */
 float oracle_rand(float x, float y) {
-    float arg = x * 12.9898f + y * 78.233f;
-    float p = oracle_sin(arg) * 43758.5453f;
+    float arg = x * ORACLE_RAND_DOT_X + y * ORACLE_RAND_DOT_Y;
+    float p = oracle_sin(arg) * ORACLE_RAND_SCALE;
     return p - floorf(p);
 }
 
@@ -201,7 +225,7 @@ static v3 ray_color(const oracle_sphere* world, int n, v3 ro, v3 rd, int max_dep
     v3 color = V(1.0f, 1.0f, 1.0f);
     for (int pass = 0; pass < max_depth; pass++) {
         (*segs)++;
-        float max_t = 1e5f, min_t = 0.001f;
+        float max_t = ORACLE_INFINITY, min_t = ORACLE_MIN_T;
         int hit = 0;
         v3 point = V(0, 0, 0), normal = V(0, 0, 0);
         const oracle_sphere* rec = NULL;
@@ -228,9 +252,11 @@ static v3 ray_color(const oracle_sphere* world, int n, v3 ro, v3 rd, int max_dep
         }
         if (!hit) { /* sky, functions.glsl:85-89 */
             v3 unit = vnormalize(rd);
-            float a = 0.5f * (unit.y + 1.0f);
-            float om = 1.0f - a;
-            v3 m = V(1.0f * om + 0.5f * a, 1.0f * om + 0.7f * a, 1.0f * om + 1.0f * a);
+            float a = ORACLE_SKY_HALF * (unit.y + ORACLE_SKY_ONE);
+            float om = 1.0f - a; /* mix(x, y, a) = x * (1 - a) + y * a */
+            v3 m = V(ORACLE_SKY_BOTTOM * om + ORACLE_SKY_TOP_R * a,
+                     ORACLE_SKY_BOTTOM * om + ORACLE_SKY_TOP_G * a,
+                     ORACLE_SKY_BOTTOM * om + ORACLE_SKY_TOP_B * a);
             return vmul(color, m);
         }
         v3 albedo = vload(rec->colour);
@@ -320,8 +346,9 @@ typedef struct {
 } render_job;
 
 /* One pixel (shader.comp:43-57) into px[4]. Accumulation (vulkancomputeraytracing_amd/csrc/
- * vcrt_math.h "Accumulation"): the samples are cut into chunks of K (restarting at every
- * progressive frame of frame_spp samples); a chunk is summed in fp32 in sample order, as the
+ * vcrt_math.h "Accumulation"): the samples are cut into quanta of G (accumulate_quantum; before
+ * round 4, and still when it is 0, chunks of K plus the tail's chunks), restarting at every
+ * progressive frame of frame_spp samples; a quantum is summed in fp32 in sample order, as the
  * reference sums (shader.comp:46-54). A single chunk (K >= spp, no progressive frames) is then
  * divided by SAMPLES_PER_PIXEL in fp32: the reference's own arithmetic (shader.comp:56).
  * Otherwise every chunk sum S is quantized to q = RN_even(S * 2^32) (|S| < 2^12; a NaN, infinite
@@ -348,7 +375,11 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
                          : 0;
     const int tail_chunk =
         cfg->accumulate_tail_chunk < tail ? cfg->accumulate_tail_chunk : tail;
-    const int single = cfg->frame_spp <= 0 && chunk >= cfg->spp && tail == 0;
+    /* round 4: the accumulation quantum G (> 0) replaces the chunk partition: runs of G samples
+     * from each frame's start, whatever the work items (vcrt.h accumulate_quantum) */
+    const int quantum = cfg->accumulate_quantum;
+    const int single = quantum > 0 ? (cfg->frame_spp <= 0 && quantum >= cfg->spp)
+                                   : (cfg->frame_spp <= 0 && chunk >= cfg->spp && tail == 0);
     double sum[3] = {0.0, 0.0, 0.0};
     v3 part = V(0.0f, 0.0f, 0.0f);
     for (int c0 = 0; c0 < cfg->spp;) {
@@ -357,7 +388,9 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
         if (block_end > cfg->spp) block_end = cfg->spp;
         const int tail_start = block_end - tail;
         int c1;
-        if (c0 < tail_start)
+        if (quantum > 0)
+            c1 = c0 + quantum < block_end ? c0 + quantum : block_end;
+        else if (c0 < tail_start)
             c1 = c0 + chunk < tail_start ? c0 + chunk : tail_start;
         else
             c1 = c0 + tail_chunk < block_end ? c0 + tail_chunk : block_end;
@@ -421,8 +454,8 @@ static int run_job(render_job* job, int32_t threads, uint64_t* segments) {
     float* jit = (float*)malloc(sizeof(float) * 2 * (size_t)cfg->spp);
     if (!jit) return -1;
     for (int i = 0; i < cfg->spp; i++) {
-        jit[2 * i] = -0.5f + oracle_rand((float)i, (float)i);
-        jit[2 * i + 1] = -0.5f + oracle_rand((float)(i + 1), (float)(i + 1));
+        jit[2 * i] = ORACLE_JITTER_OFFSET + oracle_rand((float)i, (float)i);
+        jit[2 * i + 1] = ORACLE_JITTER_OFFSET + oracle_rand((float)(i + 1), (float)(i + 1));
     }
     job->jitter = jit;
     pthread_mutex_init(&job->lock, NULL);

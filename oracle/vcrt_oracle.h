@@ -46,11 +46,19 @@ typedef struct oracle_config {
     int32_t frame_spp;
     int32_t accumulate_tail;
     int32_t accumulate_tail_chunk;
+    int32_t accumulate_quantum; /* > 0: runs of this many samples replace the chunk partition */
 } oracle_config;
 
 /* Canonical math (see DESIGN.md "canonical math"). */
 float oracle_sin(float x);
 float oracle_rand(float x, float y);
+
+/* The reference literals the restatement uses, in this order: rand dot x, rand dot y, rand
+ * scale (functions.glsl:11), min_t (:76), infinity (globals.glsl:26), sky 0.5 and 1.0
+ * (functions.glsl:87), sky bottom 1 and top .5, .7, 1 (:88), jitter offset -0.5
+ * (shader.comp:48). */
+#define ORACLE_NCONSTANTS 12
+void oracle_reference_constants(float out[ORACLE_NCONSTANTS]);
 
 /* shader.comp:18-39 -> out[0..2]=pixel00, [3..5]=delta_u, [6..8]=delta_v, [9..11]=center,
  * [12]=focal_length, [13]=viewport_height, [14]=viewport_width. */

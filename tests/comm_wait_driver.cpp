@@ -51,6 +51,22 @@ int main() {
     const int64_t dt = vcrt::steady_ms() - t0;
     std::printf("real_clock %s %d %lld\n", name(r), polls, static_cast<long long>(dt));
 
+    // a slow but alive peer: base deadline 50 ms, this rank's frame 30 ms -> 50 + 121 ms; the
+    // gather completes at 150 ms (past the base deadline alone) and is done, not lost
+    polls = 0;
+    fake = 0;
+    const int64_t gt = vcrt::gather_timeout_ms(50, 30.0);
+    r = vcrt::wait_with_deadline(
+        [&] { return ++polls < 150 ? PollState::kPending : PollState::kDone; }, gt, tick);
+    std::printf("slow_peer %s %d %lld\n", name(r), polls, static_cast<long long>(gt));
+    // ... and a peer that never sends still times out at that deadline
+    polls = 0;
+    fake = 0;
+    r = vcrt::wait_with_deadline([&] { ++polls; return PollState::kPending; }, gt, tick);
+    std::printf("lost_peer %s %d\n", name(r), polls);
+    std::printf("gather_ms %lld %lld\n", static_cast<long long>(vcrt::gather_timeout_ms(120000, 0.0)),
+                static_cast<long long>(vcrt::gather_timeout_ms(120000, 2670.5)));
+
     // the environment override of the default deadline
     std::printf("default_ms %lld\n", static_cast<long long>(vcrt::comm_timeout_ms()));
     return 0;

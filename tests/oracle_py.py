@@ -33,6 +33,7 @@ class OracleConfig(ctypes.Structure):
         ("frame_spp", ctypes.c_int32),
         ("accumulate_tail", ctypes.c_int32),
         ("accumulate_tail_chunk", ctypes.c_int32),
+        ("accumulate_quantum", ctypes.c_int32),
     ]
 
 
@@ -70,6 +71,8 @@ class Oracle:
         L.oracle_encode_srgb8.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         L.oracle_scene_generator_text.restype = ctypes.c_size_t
         L.oracle_scene_generator_text.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_reference_constants.restype = None
+        L.oracle_reference_constants.argtypes = [ctypes.c_void_p]
         L.oracle_scene_random_spheres.restype = ctypes.c_int32
         L.oracle_scene_random_spheres.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_void_p,
                                                                          ctypes.c_int32]
@@ -81,11 +84,22 @@ class Oracle:
     def rand(self, x: float, y: float) -> float:
         return self.lib.oracle_rand(x, y)
 
+    CONSTANT_NAMES = ("rand_dot_x", "rand_dot_y", "rand_scale", "min_t", "infinity", "sky_half",
+                      "sky_one", "sky_bottom", "sky_top_r", "sky_top_g", "sky_top_b",
+                      "jitter_offset")
+
+    def reference_constants(self) -> dict:
+        """The reference literals the oracle's restatement uses (vcrt_oracle.h order)."""
+        out = np.zeros(len(self.CONSTANT_NAMES), dtype=np.float32)
+        self.lib.oracle_reference_constants(out.ctypes.data)
+        return dict(zip(self.CONSTANT_NAMES, out))
+
     @staticmethod
     def config(width, height, spp, max_depth, lookfrom=(13, 2, 3), lookat=(0, 0, 0),
                vup=(0, 1, 0), vfov=20.0, chunk=0, frame_spp=0, tail=0,
-               tail_chunk=0) -> OracleConfig:
+               tail_chunk=0, quantum=0) -> OracleConfig:
         c = OracleConfig()
+        c.accumulate_quantum = quantum
         c.accumulate_chunk = chunk
         c.frame_spp = frame_spp
         c.accumulate_tail = tail
@@ -104,9 +118,11 @@ class Oracle:
 
     @staticmethod
     def partition(stats: dict) -> dict:
-        """config() keywords for the chunk partition a render used (its stats)."""
+        """config() keywords for the accumulation a render used (its stats): the quantum G (round
+        4), with the work partition beside it (which no longer changes the image)."""
         return dict(chunk=stats["accumulate_chunk"], tail=stats["accumulate_tail"],
-                    tail_chunk=stats["accumulate_tail_chunk"])
+                    tail_chunk=stats["accumulate_tail_chunk"],
+                    quantum=stats["accumulate_quantum"])
 
     # ---- render ----
     def render(self, cfg: OracleConfig, spheres: np.ndarray, rows=None, threads: int = 0):

@@ -40,6 +40,15 @@ def test_wait_outcomes(driver):
     assert r["default_ms"] == ["120000"]
 
 
+def test_gather_deadline_scales_with_frame_time(driver):
+    """the gather's deadline covers the peers' renders, so a frame slower than the
+    base deadline must not be reported as a lost peer; a peer that never sends still times out."""
+    r = run(driver)
+    assert r["slow_peer"] == ["done", "150", "171"]
+    assert r["lost_peer"] == ["timeout", "171"]
+    assert r["gather_ms"] == ["120001", str(120000 + int(4 * 2670.5 + 1))]
+
+
 def test_timeout_from_environment(driver):
     assert run(driver, VCRT_COMM_TIMEOUT_MS="2500")["default_ms"] == ["2500"]
     assert run(driver, VCRT_COMM_TIMEOUT_MS="0")["default_ms"] == ["120000"]

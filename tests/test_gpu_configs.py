@@ -101,28 +101,28 @@ def test_final_scene_configs_row_subset(oracle, name):
 
 
 def test_c4_sharded_eight_ways_equals_one_gpu(oracle):
-    """C4's 8-GPU decomposition rendered rank by rank on one GPU: every rank's tiles, gathered
-    and re-interleaved by vcrt_assemble, give the 1-GPU frame with the same accumulation chunk
-    bit for bit (chunk sums are combined exactly, in whatever order the ranks finish them)."""
+    """C4's 8-GPU decomposition rendered rank by rank on one GPU, with DEFAULT descs on both
+    sides: every rank's tiles, gathered and re-interleaved by vcrt_assemble, give the default
+    1-GPU frame bit for bit. The two use different work items (the 8-way shares take smaller
+    chunks), but the image depends on the accumulation quantum alone (round 4): quantum sums are
+    combined exactly, in whatever order the ranks finish them."""
     import torch
     from vulkancomputeraytracing_amd import distributed as D
     scene, w, h, spp, depth = CONFIGS["c4"]
     world = 8
+    d1 = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp)
     d8 = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
-    k8 = vc.renderer.work_chunk(d8)
-    t8, kt8 = vc.renderer.work_tail(d8)
-    assert (k8, t8, kt8) == (16, 128, 4)
-    # the 8-way default partition (head chunk and tail) on one GPU
-    full, st1 = render_full("c4", accumulate_chunk=k8, accumulate_tail=t8,
-                            accumulate_tail_chunk=kt8)
+    assert vc.renderer.work_quantum(d1) == vc.renderer.work_quantum(d8) == 16
+    assert vc.renderer.work_chunk(d1) != vc.renderer.work_chunk(d8)  # 64 against 16
+    full, st1 = render_full("c4")  # the default 1-GPU frame
     pad = D.tiles_per_rank(w, h, world)
     gathered = torch.zeros((world * pad * 64, 4), dtype=torch.float32, device="cuda:0")
     segs = 0
     for rank in range(world):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
-                             device=0, rank=rank, world_size=world)  # default chunk: k8
+                             device=0, rank=rank, world_size=world)  # the 8-way default
         with vc.Renderer(desc, scene) as r:
-            assert oracle.partition(r.stats()) == oracle.partition(st1)
+            assert r.stats()["accumulate_quantum"] == st1["accumulate_quantum"]
             r.set_framebuffer_device(gathered[rank * pad * 64:].data_ptr(), pad * 64 * 16)
             r.draw_next_frame()
             segs += r.stats()["segments"]
@@ -154,7 +154,7 @@ def test_cpp_host_api_reference_configuration_whole_frame(oracle, tmp_path, conf
     configuration: 1280x720, 1 spp, depth 50, its camera and its world[] (globals.glsl:9-24,
     29-518; Common.hpp:23-24). Without options vcrt_render sets nothing, exactly as the
     reference's main(); with them it goes through SetRenderDescription / SetRenderScene. At
-    1 spp the GPU runs one chunk per pixel -- the reference's own arithmetic (sum, then divide
+    1 spp the GPU runs one quantum per pixel -- the reference's own arithmetic (sum, then divide
     by SAMPLES_PER_PIXEL) -- so the WHOLE frame is compared bit for bit with the oracle, over
     two DrawNextFrame calls (each frame re-renders the same image, Linux.cpp:362-366)."""
     import re

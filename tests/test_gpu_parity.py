@@ -20,23 +20,32 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def gpu_render(scene, width, height, spp, depth, variant=vc.KERNEL_AUTO, rank=0, world=1,
-               frames=1, scene_arr=None, chunk=0):
+               frames=1, scene_arr=None, chunk=0, quantum=0):
     desc = vc.RenderDesc(width=width, height=height, samples_per_pixel=spp, max_depth=depth,
                          kernel_variant=variant, rank=rank, world_size=world, device=0,
-                         accumulate_chunk=chunk)
+                         accumulate_chunk=chunk, accumulate_quantum=quantum)
     with vc.Renderer(desc, scene_arr if scene_arr is not None else scene) as r:
         for _ in range(frames):
             r.draw_next_frame()
         return r.read_framebuffer(), r.stats()
 
 
-def chunk_of(w, h, spp, chunk=0, world=1, tail=0, tail_chunk=0):
-    """The chunk partition the renderer uses, as oracle.config() keywords (C ABI vcrt_work_chunk
-    and vcrt_work_tail, no re-implementation)."""
+def chunk_of(w, h, spp, chunk=0, world=1, tail=0, tail_chunk=0, quantum=0):
+    """The accumulation quantum and the work partition the renderer uses, as oracle.config()
+    keywords (C ABI vcrt_work_quantum, vcrt_work_chunk and vcrt_work_tail, no
+    re-implementation). The oracle's image depends on the quantum alone."""
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, accumulate_chunk=chunk,
-                         world_size=world, accumulate_tail=tail, accumulate_tail_chunk=tail_chunk)
+                         world_size=world, accumulate_tail=tail, accumulate_tail_chunk=tail_chunk,
+                         accumulate_quantum=quantum)
     t, kt = vc.renderer.work_tail(desc)
-    return dict(chunk=vc.renderer.work_chunk(desc), tail=t, tail_chunk=kt)
+    return dict(chunk=vc.renderer.work_chunk(desc), tail=t, tail_chunk=kt,
+                quantum=vc.renderer.work_quantum(desc))
+
+
+def seq_quantum(spp):
+    """The smallest quantum (a power of two) that covers spp samples: one quantum per pixel,
+    the reference's sequential sum and division (shader.comp:46-56)."""
+    return 1 << (spp - 1).bit_length()
 
 
 def bits(a):
@@ -77,7 +86,7 @@ def expected_variant(variant, nspheres):
 @pytest.mark.parametrize("scene,w,h,spp,depth", CASES)
 def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
     got, st = gpu_render(scene, w, h, spp, depth, variant)
-    # default work split: the oracle sums in the same order (chunks of accumulate_chunk)
+    # default accumulation: the oracle sums in the same quanta
     assert oracle.partition(st) == chunk_of(w, h, spp)
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth,
                                                   **oracle.partition(st)),
@@ -89,16 +98,19 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("scene,w,h,spp,depth,chunk", [
-    ("final", 64, 36, 64, 10, 16),   # 4 chunks
-    ("final", 48, 30, 40, 10, 0),    # default chunk for a tiny frame: 4 (10 chunks)
-    ("three", 72, 40, 96, 8, 7),     # 14 chunks, last one of 5
-    ("final", 40, 24, 33, 10, 33),   # one chunk = the reference's sequential order
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,quantum", [
+    ("final", 64, 36, 64, 10, 16, 0),   # 4 items of one quantum (16)
+    ("final", 48, 30, 40, 10, 0, 0),    # the default for a tiny frame: quanta 16 + 16 + 8
+    ("three", 72, 40, 96, 8, 7, 1),     # 14 items (the last of 5), every sample a quantum
+    ("final", 64, 36, 48, 10, 32, 4),   # items of 8 quanta (the last of 4): mid-item retires
+    ("three", 40, 24, 40, 8, 0, 8),     # 5 quanta of 8 inside items of 32 and 8
+    ("final", 40, 24, 33, 10, 33, 64),  # one quantum = the reference's sequential order
 ])
-def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, variant):
-    k = chunk_of(w, h, spp, chunk)
+def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, quantum,
+                                                variant):
+    k = chunk_of(w, h, spp, chunk, quantum=quantum)
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
-    got, st = gpu_render(scene, w, h, spp, depth, variant, chunk=chunk)
+    got, st = gpu_render(scene, w, h, spp, depth, variant, chunk=chunk, quantum=quantum)
     assert oracle.partition(st) == k
     assert_bitwise(got, want, f"{scene} spp{spp} chunk{k}")
     assert st["segments"] == want_segs
@@ -110,21 +122,26 @@ def test_chunked_accumulation_bitwise_vs_oracle(oracle, scene, w, h, spp, depth,
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,tail,tail_chunk", [
-    ("final", 64, 36, 40, 10, 8, 12, 5),   # head 28 = 8+8+8+4, tail 12 = 5+5+2
-    ("three", 72, 40, 33, 8, 16, 9, 1),    # a tail of single samples
-    ("final", 40, 24, 20, 10, 16, 6, 4),   # the head one chunk of 14
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,tail,tail_chunk,quantum", [
+    ("final", 64, 36, 40, 10, 8, 12, 5, 1),   # head 28 = 8+8+8+4, tail 12 = 5+5+2
+    ("three", 72, 40, 33, 8, 16, 9, 1, 1),    # a tail of single samples
+    ("final", 40, 24, 20, 10, 16, 6, 4, 1),   # the head one chunk of 14
+    ("final", 64, 36, 40, 10, 16, 16, 4, 4),  # head 24 = 16+8, tail 16 = 4 x 4: whole quanta
+    ("three", 72, 40, 36, 8, 8, 10, 2, 4),    # rounded to quanta: head 24, tail 12 in 4s
 ])
 def test_tail_partition_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, chunk, tail,
-                                          tail_chunk, variant):
-    """The tail of the chunk partition (the last samples of every pixel in their own items,
-    handed out after the head): the oracle's partition, bit for bit."""
-    k = chunk_of(w, h, spp, chunk, tail=tail, tail_chunk=tail_chunk)
-    assert (k["tail"], k["tail_chunk"]) == (tail, tail_chunk)
+                                          tail_chunk, quantum, variant):
+    """The tail of the work partition (the last samples of every pixel in their own items,
+    handed out after the head), items holding whole quanta: the oracle's image, bit for bit."""
+    k = chunk_of(w, h, spp, chunk, tail=tail, tail_chunk=tail_chunk, quantum=quantum)
+    if quantum == 1:
+        assert (k["tail"], k["tail_chunk"]) == (tail, tail_chunk)
+    else:  # whole quanta: the head ends on a quantum boundary
+        assert (spp - k["tail"]) % quantum == 0 and k["tail_chunk"] % quantum == 0
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
                          kernel_variant=variant, accumulate_chunk=chunk, accumulate_tail=tail,
-                         accumulate_tail_chunk=tail_chunk)
+                         accumulate_tail_chunk=tail_chunk, accumulate_quantum=quantum)
     with vc.Renderer(desc, scene) as r:
         r.draw_next_frame()
         got, st = r.read_framebuffer(), r.stats()
@@ -138,7 +155,7 @@ def test_tail_partition_progressive_and_sharded(oracle, world):
     """Progressive frames with a tail in each frame, rendered in `world` shards: every rank's
     pixels equal the oracle's at every frame."""
     w, h, spp, depth, frames = 56, 32, 10, 10, 2
-    part = dict(chunk=3, tail=4, tail_chunk=2)
+    part = dict(chunk=3, tail=4, tail_chunk=2, quantum=1)
     m = vc.tile_pixel_map(w, h, world)
     sc = oracle.scene("final")
     wants = [oracle.render(oracle.config(w, h, (f + 1) * spp, depth, frame_spp=spp, **part),
@@ -146,7 +163,8 @@ def test_tail_partition_progressive_and_sharded(oracle, world):
     for rank in range(world):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
                              device=0, rank=rank, world_size=world, progressive=True,
-                             accumulate_chunk=3, accumulate_tail=4, accumulate_tail_chunk=2)
+                             accumulate_chunk=3, accumulate_tail=4, accumulate_tail_chunk=2,
+                             accumulate_quantum=1)
         mine = m[..., 0] == rank
         with vc.Renderer(desc, "final") as r:
             assert oracle.partition(r.stats()) == part
@@ -164,8 +182,8 @@ def test_golden_oracle_images():
     from tests.golden.make_golden import IMAGES
     data = np.load(os.path.join(GOLDEN, "oracle_images.npz"))
     for name, scene, w, h, spp, depth in IMAGES:
-        # the goldens hold the reference's sequential sum: one chunk per pixel
-        got, st = gpu_render(scene, w, h, spp, depth, chunk=spp)
+        # the goldens hold the reference's sequential sum: one quantum per pixel
+        got, st = gpu_render(scene, w, h, spp, depth, quantum=seq_quantum(spp))
         assert_bitwise(got, data[name], name)
         assert st["segments"] == int(data[name + "__segments"][0])
 
@@ -238,11 +256,13 @@ def test_flat_scan_boxes_in_lds(oracle, monkeypatch, scene, w, h, spp, depth, ch
         sc = culling_torture_scene()
     else:
         sc = scene
-    k = chunk_of(w, h, spp, chunk)
+    quantum = 1 if chunk else 0  # explicit items: a quantum per sample, several items per pixel
+    k = chunk_of(w, h, spp, chunk, quantum=quantum)
     oscene = oracle.scene(sc) if isinstance(sc, str) else sc
     want, segs = oracle.render(oracle.config(w, h, spp, depth, **k, **cfg), oscene)
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
-                         kernel_variant=vc.KERNEL_CULL_FLAT, accumulate_chunk=chunk, **cfg)
+                         kernel_variant=vc.KERNEL_CULL_FLAT, accumulate_chunk=chunk,
+                         accumulate_quantum=quantum, **cfg)
     with vc.Renderer(desc, sc) as r:
         r.draw_next_frame()
         got, st = r.read_framebuffer(), r.stats()
@@ -318,11 +338,13 @@ def test_culled_scan_torture_scene(oracle, w, h, spp, depth, chunk):
     sc = culling_torture_scene()
     assert len(sc) >= 16
     cfg = dict(lookfrom=(6, 2.5, 5), lookat=(0, 0.6, 0), vfov=45)
-    k = chunk_of(w, h, spp, chunk)
+    quantum = 1 if chunk else 0
+    k = chunk_of(w, h, spp, chunk, quantum=quantum)
     want, segs = oracle.render(oracle.config(w, h, spp, depth, **k, **cfg), sc)
     for variant in (vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE, vc.KERNEL_CULL_FLAT):
         desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
-                             device=0, kernel_variant=variant, accumulate_chunk=chunk, **cfg)
+                             device=0, kernel_variant=variant, accumulate_chunk=chunk,
+                             accumulate_quantum=quantum, **cfg)
         with vc.Renderer(desc, sc) as r:
             r.draw_next_frame()
             got, st = r.read_framebuffer(), r.stats()
@@ -425,10 +447,11 @@ def test_sharded_tiles_reassemble_bitwise(world):
 def test_sharded_chunked_render_matches_oracle(oracle):
     # a rank shard with several sample chunks (resolve kernel on packed tiles)
     w, h, spp, depth, world = 64, 40, 24, 10, 3
-    want, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=8), oracle.scene("final"))
+    want, _ = oracle.render(oracle.config(w, h, spp, depth, quantum=8), oracle.scene("final"))
     m = vc.tile_pixel_map(w, h, world)
     for rank in range(world):
-        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world, chunk=8)
+        part, st = gpu_render("final", w, h, spp, depth, rank=rank, world=world, chunk=8,
+                              quantum=8)
         mine = m[..., 0] == rank
         assert_bitwise(part.reshape(-1, 4)[m[..., 1][mine]], want[mine], f"rank {rank}")
 
@@ -510,11 +533,11 @@ def test_srgb8_encode_bitwise(oracle):
     assert np.array_equal(srgb, oracle.encode_srgb8(want))
 
 
-@pytest.mark.parametrize("spp,chunk", [(4, 0), (6, 4), (3, 1)])
-def test_progressive_frames_bitwise(oracle, spp, chunk):
+@pytest.mark.parametrize("spp,chunk,quantum", [(4, 0, 0), (6, 4, 2), (3, 1, 1), (40, 0, 0)])
+def test_progressive_frames_bitwise(oracle, spp, chunk, quantum):
     w, h, depth, frames = 48, 30, 10, 3
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
-                         progressive=True, accumulate_chunk=chunk)
+                         progressive=True, accumulate_chunk=chunk, accumulate_quantum=quantum)
     scene = oracle.scene("final")
     with vc.Renderer(desc, "final") as r:
         k = oracle.partition(r.stats())
@@ -558,7 +581,10 @@ def test_sin_fast_exhaustive():
 def test_bench_multirank_gather_bitwise():
     """bench.py's N-rank path end to end on one GPU (3 ranks rendering their tile shares in
     turn, gloo standing in for RCCL, which refuses two ranks on one device): the frame gathered
-    to rank 0 and re-interleaved by vcrt_assemble is bit-identical to a 1-GPU render."""
+    to rank 0 and re-interleaved by vcrt_assemble is bit-identical to a default 1-GPU render.
+    At N > 1 the line validates itself without --validate (the driver's first
+    multi-GPU run must prove its gather): bitwise_vs_1gpu, the oracle rows, the per-rank kernel
+    times and gather_ms are in the JSON."""
     import json
     import socket
     import subprocess
@@ -571,7 +597,7 @@ def test_bench_multirank_gather_bitwise():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(root, "bench.py"),
            "--gpus", "3", "--steps", "1", "--warmup", "0", "--width", "200", "--height", "120",
-           "--spp", "8", "--depth", "10", "--scene", "final", "--no-cpu-baseline", "--validate"]
+           "--spp", "40", "--depth", "10", "--scene", "final", "--no-cpu-baseline"]
     out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stderr[-2000:]
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
@@ -579,6 +605,10 @@ def test_bench_multirank_gather_bitwise():
     assert res["n_gpus"] == 3
     assert res["validated"]["bitwise_vs_1gpu"] is True
     assert res["validated"]["bitwise_vs_oracle"] is True
+    assert res["validated"]["quantum"] == [16, 16]
+    pr = res["per_rank_kernel_ms"]
+    assert len(pr["ranks"]) == 3 and 0 < pr["min"] <= pr["max"]
+    assert "gather_ms" in res
 
 
 def test_bench_rccl_init_failure_falls_back_to_gloo():
@@ -723,23 +753,24 @@ def test_stats_name_the_launched_kernel(scene, variant, kernel):
     assert st["kernel"] == kernel
 
 
-@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,tail,tail_chunk,ring", [
-    ("final", 64, 36, 40, 10, 8, 12, 5, "0"),       # ring off: chunk sums straight to memory
-    ("final", 64, 36, 40, 10, 8, 12, 5, "8"),       # a small ring: entries recycled often
-    ("three", 37, 23, 48, 8, 4, 0, 0, "1"),         # ragged edge tiles, 12 chunks per pixel
-    ("final", 50, 30, 33, 10, 7, 0, 0, "1"),        # 5 chunks: blocks straddle pixels
-    ("stress4096", 40, 24, 20, 12, 4, 8, 2, "1"),  # the boxes-in-LDS kernel's ring
+@pytest.mark.parametrize("scene,w,h,spp,depth,chunk,tail,tail_chunk,quantum,ring", [
+    ("final", 64, 36, 40, 10, 8, 12, 5, 1, "0"),      # ring off: sums straight to memory
+    ("final", 64, 36, 40, 10, 8, 12, 5, 1, "8"),      # a small ring: entries recycled often
+    ("three", 37, 23, 48, 8, 4, 0, 0, 4, "1"),        # ragged edge tiles, 12 items per pixel
+    ("final", 50, 30, 33, 10, 7, 0, 0, 1, "1"),       # 5 items: blocks straddle pixels
+    ("final", 50, 30, 64, 10, 32, 0, 0, 8, "1"),      # four quanta per item into one entry
+    ("stress4096", 40, 24, 20, 12, 4, 8, 2, 2, "1"),  # the boxes-in-LDS kernel's ring
 ])
 def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth, chunk, tail,
-                                   tail_chunk, ring):
-    """The per-wave LDS accumulation ring (tracer.hip RingEntry): chunk sums added in LDS and
-    flushed per pixel give the same exact sums as adding every chunk sum to global memory."""
+                                   tail_chunk, quantum, ring):
+    """The per-wave LDS accumulation ring (tracer.hip RingEntry): quantum sums added in LDS and
+    flushed per pixel give the same exact sums as adding every quantum sum to global memory."""
     monkeypatch.setenv("VCRT_ACCUM_RING", ring)
-    k = chunk_of(w, h, spp, chunk, tail=tail, tail_chunk=tail_chunk)
+    k = chunk_of(w, h, spp, chunk, tail=tail, tail_chunk=tail_chunk, quantum=quantum)
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth, **k), oracle.scene(scene))
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
                          accumulate_chunk=chunk, accumulate_tail=tail,
-                         accumulate_tail_chunk=tail_chunk)
+                         accumulate_tail_chunk=tail_chunk, accumulate_quantum=quantum)
     with vc.Renderer(desc, scene) as r:
         r.draw_next_frame()
         got, st = r.read_framebuffer(), r.stats()

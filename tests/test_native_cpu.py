@@ -33,15 +33,121 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) == set(N.SIGNATURES), "ctypes signatures out of sync with vcrt.h"
 
 
+def _constants():
+    return json.load(open(os.path.join(GOLDEN, "reference_constants.json")))["constants"]
+
+
+def _f32bits(x):
+    return int(np.float32(x).view(np.uint32))
+
+
+def _bits_of(entry):
+    b = entry["f32_bits"]
+    return [int(v, 16) for v in b] if isinstance(b, list) else int(b, 16)
+
+
 def test_struct_layouts():
     assert ctypes.sizeof(N.vcrt_sphere) == 40  # GLSL struct sphere
     assert ctypes.sizeof(N.vcrt_camera) == 40
     d = N.vcrt_render_desc()
     assert N.lib().vcrt_default_desc(ctypes.byref(d)) == 0
     assert d.struct_size == ctypes.sizeof(N.vcrt_render_desc)
-    assert (d.width, d.height, d.samples_per_pixel, d.max_depth) == (1280, 720, 1, 50)
-    assert list(d.camera.lookfrom) == [13, 2, 3] and d.camera.vfov == 20
     assert (d.rank, d.world_size) == (0, 1)
+
+
+def test_default_desc_equals_reference_configuration():
+    """vcrt_default_desc (and the Python RenderDesc defaults) equal the reference's compile-time
+    configuration as parsed from globals.glsl:9-24 (the `#if 0` resolved to SAMPLES_PER_PIXEL
+    1) into tests/golden/reference_constants.json -- not a hand-typed copy."""
+    c = _constants()
+    d = N.vcrt_render_desc()
+    assert N.lib().vcrt_default_desc(ctypes.byref(d)) == 0
+    assert (d.width, d.height, d.samples_per_pixel, d.max_depth) == (
+        c["IMAGE_WIDTH"]["value"], c["IMAGE_HEIGHT"]["value"], c["SAMPLES_PER_PIXEL"]["value"],
+        c["MAX_RECURSION_LEVEL"]["value"])
+    for name in ("lookfrom", "lookat", "vup"):
+        got = [_f32bits(v) for v in getattr(d.camera, name)]
+        assert got == _bits_of(c["camera_" + name]), name
+    assert _f32bits(d.camera.vfov) == _bits_of(c["camera_vfov"])
+    py = vc.RenderDesc()
+    assert (py.width, py.height, py.samples_per_pixel, py.max_depth) == (
+        d.width, d.height, d.samples_per_pixel, d.max_depth)
+    assert [_f32bits(v) for v in py.lookfrom] == _bits_of(c["camera_lookfrom"])
+    assert [_f32bits(v) for v in py.lookat] == _bits_of(c["camera_lookat"])
+    assert [_f32bits(v) for v in py.vup] == _bits_of(c["camera_vup"])
+    assert _f32bits(py.vfov) == _bits_of(c["camera_vfov"])
+    # include/Common.hpp keeps the reference's window constants (its Common.hpp:23-25)
+    text = open(os.path.join(ROOT, "include", "Common.hpp")).read()
+    for name in ("WINDOW_WIDTH", "WINDOW_HEIGHT", "RENDER_ITERATION"):
+        m = re.search(r"constexpr\s+auto\s+%s\s*=\s*(\d+)\s*;" % name, text)
+        assert m and int(m.group(1)) == c[name]["value"], name
+
+
+# the product's named literals (csrc/vcrt_math.h) -> the fixture entry and element they pin
+_MATH_CONSTANTS = {
+    "kRandDotX": ("rand_dot", 0), "kRandDotY": ("rand_dot", 1), "kRandScale": ("rand_scale", None),
+    "kMinT": ("min_t", None), "kInfinity": ("infinity", None), "kSkyHalf": ("sky_blend", 0),
+    "kSkyOne": ("sky_blend", 1), "kSkyBottom": ("sky_bottom", 0), "kSkyTopR": ("sky_top", 0),
+    "kSkyTopG": ("sky_top", 1), "kSkyTopB": ("sky_top", 2), "kJitterOffset": ("jitter_offset", 0),
+    "kRefVfov": ("camera_vfov", None),
+}
+_ORACLE_CONSTANTS = {
+    "rand_dot_x": ("rand_dot", 0), "rand_dot_y": ("rand_dot", 1), "rand_scale": ("rand_scale", None),
+    "min_t": ("min_t", None), "infinity": ("infinity", None), "sky_half": ("sky_blend", 0),
+    "sky_one": ("sky_blend", 1), "sky_bottom": ("sky_bottom", 0), "sky_top_r": ("sky_top", 0),
+    "sky_top_g": ("sky_top", 1), "sky_top_b": ("sky_top", 2), "jitter_offset": ("jitter_offset", 0),
+}
+
+
+def _want_bits(c, key):
+    name, i = key
+    b = _bits_of(c[name])
+    return b if i is None else b[i]
+
+
+def _strtof(text):
+    libc = ctypes.CDLL(None)
+    libc.strtof.restype = ctypes.c_float
+    libc.strtof.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    return float(libc.strtof(text.rstrip("f").encode(), None))
+
+
+def test_reference_literals_pinned(oracle):
+    """Every reference literal on the hot path -- rand's coefficients (functions.glsl:11), min_t
+    (:76), infinity (globals.glsl:26), the sky blend (functions.glsl:87-88), the jitter offset
+    (shader.comp:48) and the default camera -- is defined once in the product (vcrt_math.h) and
+    once in the oracle, and both equal the values parsed from the reference files, bit for bit.
+    tracer.hip spells none of them as a literal."""
+    c = _constants()
+    text = open(os.path.join(ROOT, "vulkancomputeraytracing_amd", "csrc", "vcrt_math.h")).read()
+    num = r"[-+]?(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][-+]?[0-9]+)?f?"
+    for name, key in _MATH_CONSTANTS.items():
+        m = re.search(r"\b%s\s*=\s*(%s)\s*[,;]" % (name, num), text)
+        assert m, name
+        assert _f32bits(_strtof(m.group(1))) == _want_bits(c, key), name
+    for name in ("Lookfrom", "Lookat", "Vup"):
+        m = re.search(r"\bkRef%s\[3\]\s*=\s*\{([^}]*)\}" % name, text)
+        got = [_f32bits(_strtof(v.strip())) for v in m.group(1).split(",")]
+        assert got == _bits_of(c["camera_" + name.lower()]), name
+    for name, want in (("kRefSamplesPerPixel", "SAMPLES_PER_PIXEL"),
+                       ("kRefMaxRecursion", "MAX_RECURSION_LEVEL"),
+                       ("kRefImageWidth", "IMAGE_WIDTH"), ("kRefImageHeight", "IMAGE_HEIGHT")):
+        m = re.search(r"\b%s\s*=\s*(\d+)\s*[,;]" % name, text)
+        assert m and int(m.group(1)) == c[want]["value"], name
+    got = oracle.reference_constants()
+    for name, key in _ORACLE_CONSTANTS.items():
+        assert _f32bits(got[name]) == _want_bits(c, key), name
+    # the oracle's default camera (tests/oracle_py.py config) is the reference's too
+    import inspect
+    dflt = {k: v.default for k, v in inspect.signature(oracle.config).parameters.items()}
+    for name in ("lookfrom", "lookat", "vup"):
+        assert [_f32bits(v) for v in dflt[name]] == _bits_of(c["camera_" + name]), name
+    assert _f32bits(dflt["vfov"]) == _bits_of(c["camera_vfov"])
+    assert c["max_t_is_infinity"]["value"] is True
+    hip = open(os.path.join(ROOT, "vulkancomputeraytracing_amd", "csrc", "tracer.hip")).read()
+    hip = re.sub(r"//[^\n]*", "", hip)
+    for lit in ("12.9898", "78.233", "43758", "0.001f", "1e5f", "0.7f", "100000"):
+        assert lit not in hip, lit
 
 
 def test_product_canonical_math_equals_oracle(oracle):
@@ -178,15 +284,45 @@ def test_srgb8_thresholds_agree_with_oracle(oracle):
     assert np.array_equal(enc[:, 1], np.arange(0, 255, dtype=np.uint8))
 
 
+def _quantum_rule(spp):
+    q = 16
+    while -(-spp // q) > 512:
+        q *= 2
+    return q
+
+
+@pytest.mark.parametrize("spp", [1, 3, 16, 64, 256, 1024, 4096, 8192, 8193, 100000])
+def test_work_quantum_rule(spp):
+    """vcrt_work_quantum (the accumulation quantum G; host only): 16, doubled while a pixel would
+    take more than 512 quanta -- the same for every world size and rank (so the default image
+    does not depend on the number of GPUs); an explicit power of two is taken as given, anything
+    else is an invalid desc."""
+    for world in (1, 2, 3, 8):
+        for rank in range(world):
+            d = vc.RenderDesc(width=1920, height=1080, samples_per_pixel=spp, rank=rank,
+                              world_size=world)
+            assert vc.renderer.work_quantum(d) == _quantum_rule(spp)
+    assert vc.renderer.work_quantum(vc.RenderDesc(samples_per_pixel=spp, accumulate_quantum=4)) == 4
+    lib = N.lib()
+    for bad in (3, 12, -2):
+        d = vc.RenderDesc(samples_per_pixel=spp, accumulate_quantum=bad).to_c()
+        assert lib.vcrt_work_quantum(ctypes.byref(d)) == N.VK_ERROR_INITIALIZATION_FAILED
+
+
+def _round_up(x, q):
+    return -(-x // q) * q
+
+
 @pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (37, 23),
                                  (1, 1)])
 @pytest.mark.parametrize("spp", [1, 3, 16, 64, 256, 1024, 4096, 100000])
 def test_work_chunk_rule(w, h, spp):
-    """vcrt_work_chunk (the accumulation chunk vcrt_begin uses; host only): the same for every
-    rank of a sharded frame, at most spp, at most 512 chunks per pixel, >= 4 unless spp is
-    smaller, and an explicit accumulate_chunk is taken as given. Checked against the rule
-    restated here (64, halved while the largest rank has < 2^24 - 2^21 items, down to 16, or to
-    32 for frames of fewer than 2^22 items at 32)."""
+    """vcrt_work_chunk (the head's samples per work item; host only): the same for every rank of
+    a sharded frame, at most spp, whole quanta, and an explicit accumulate_chunk rounded up to
+    whole quanta. Checked against the rule restated here (64, halved while the largest rank has
+    < 2^24 - 2^21 items, down to 16, or to 32 for frames of fewer than 2^22 items at 32; at least
+    spp / 512; then whole quanta)."""
+    q = _quantum_rule(spp)
     for world in (1, 2, 3, 8):
         ks = {vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
                                                    rank=rank, world_size=world))
@@ -194,17 +330,19 @@ def test_work_chunk_rule(w, h, spp):
         assert len(ks) == 1
         k = ks.pop()
         assert 1 <= k <= spp
-        assert -(-spp // k) <= 512
-        assert k == spp or k >= 16
+        assert k == spp or k % q == 0
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
         want = 64
         floor = 32 if slots * -(-spp // 32) < (1 << 22) else 16  # small frames stop at 32
         while want > floor and slots * -(-spp // want) < (1 << 24) - (1 << 21):
             want //= 2
-        assert k == min(max(want, -(-spp // 512)), spp)
+        assert k == min(_round_up(max(want, -(-spp // 512)), q), spp)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
                                                     world_size=world, accumulate_chunk=7)) \
-            == min(7, spp)
+            == min(_round_up(7, q), spp)
+        assert vc.renderer.work_chunk(vc.RenderDesc(
+            width=w, height=h, samples_per_pixel=spp, world_size=world, accumulate_chunk=7,
+            accumulate_quantum=1)) == min(7, spp)
     if (w, h, spp) == (1920, 1080, 1024):  # the bench config: K = 64 / 64 / 32 / 16 on 1/2/4/8
         for world, want in ((1, 64), (2, 64), (4, 32), (8, 16)):
             assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
@@ -214,12 +352,12 @@ def test_work_chunk_rule(w, h, spp):
 @pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (1, 1)])
 @pytest.mark.parametrize("spp", [1, 16, 64, 256, 1024, 4096, 32768, 100000])
 def test_work_tail_rule(w, h, spp):
-    """vcrt_work_tail (the tail of the chunk partition; host only): the same for every rank,
+    """vcrt_work_tail (the tail of the work partition; host only): the same for every rank,
     restated here -- T = 6 * K * 327680 / (64 * the largest rank's tiles) to the nearest power of
-    two, items of max(4, K / 8) samples, none when 4 T > spp or K >= spp, the items grown until
-    head and tail take at most 512 chunks per pixel -- and explicit values (capped below spp) or
-    -1 (none) taken as given."""
+    two, none when 4 T > spp or K >= spp, the head ending on a quantum boundary, items of one
+    quantum -- and explicit values (capped below spp, rounded to whole quanta) or -1 (none)."""
     import math
+    q = _quantum_rule(spp)
     for world in (1, 2, 3, 8):
         parts = set()
         for rank in range(world):
@@ -235,34 +373,32 @@ def test_work_tail_rule(w, h, spp):
             want = 1 << round(math.log2(raw))
             if 4 * want > spp:
                 want = 0
-        want_kt = min(max(4, k // 8), want) if want else 0
         if want:
-            room = 512 - -(-(spp - want) // k)
-            if -(-want // want_kt) > room:
-                if room > 0:
-                    want_kt = -(-want // room)
-                else:
-                    want, want_kt = 0, 0
+            head_end = (spp - want) // q * q
+            want = spp - head_end if head_end > 0 else 0
         assert t == want
-        assert kt == want_kt
-        # what vcrt_begin accepts: at most 512 chunks per pixel, head and tail together
-        assert -(-(spp - t) // k) + (-(-t // kt) if t else 0) <= 512
+        assert kt == (min(q, want) if want else 0)
+        if t:
+            assert (spp - t) % q == 0
         d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world,
-                          accumulate_chunk=k, accumulate_tail=5, accumulate_tail_chunk=2)
+                          accumulate_chunk=k, accumulate_tail=5, accumulate_tail_chunk=2,
+                          accumulate_quantum=1)
         t5 = vc.renderer.work_tail(d)
-        assert t5 == ((0, 0) if k >= spp else (min(5, spp - 1), min(2, min(5, spp - 1))))
+        k1 = vc.renderer.work_chunk(d)
+        assert t5 == ((0, 0) if k1 >= spp else (min(5, spp - 1), min(2, min(5, spp - 1))))
         d.accumulate_tail = -1
         assert vc.renderer.work_tail(d) == (0, 0)
     if (w, h, spp) == (1920, 1080, 1024):  # the bench config on 1/2/4/8 GPUs
-        for world, want in ((1, (64, 64, 8)), (2, (64, 128, 8)), (4, (32, 128, 4)),
-                            (8, (16, 128, 4))):
+        for world, want in ((1, (64, 64, 16)), (2, (64, 128, 16)), (4, (32, 128, 16)),
+                            (8, (16, 128, 16))):
             d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
             assert (vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d) == want
 
 
 def test_oracle_tail_partition(oracle):
-    """The oracle's tail: a tail cut on the head's own chunk boundaries into chunks of the same
-    size is the same partition (same bits); another cut moves the image by rounding only."""
+    """The oracle's legacy chunk partition (accumulate_quantum 0): a tail cut on the head's own
+    chunk boundaries into chunks of the same size is the same partition (same bits); another cut
+    moves the image by rounding only."""
     sc = oracle.scene("three")
     w, h, spp, depth = 24, 14, 24, 6
     plain, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=4), sc)
@@ -276,6 +412,27 @@ def test_oracle_tail_partition(oracle):
                                           tail_chunk=4), sc)
     prog0, _ = oracle.render(oracle.config(w, h, 2 * spp, depth, chunk=4, frame_spp=spp), sc)
     assert np.array_equal(prog.view(np.uint32), prog0.view(np.uint32))
+
+
+def test_oracle_quantum_replaces_the_partition(oracle):
+    """With an accumulation quantum G the oracle's image depends on G alone: the work partition
+    (chunk, tail) no longer matters, and G equals the legacy partition of chunks of G with no
+    tail; G >= spp is the reference's sequential sum and division."""
+    sc = oracle.scene("final")
+    w, h, spp, depth = 20, 12, 40, 10
+    a, _ = oracle.render(oracle.config(w, h, spp, depth, quantum=8), sc)
+    b, _ = oracle.render(oracle.config(w, h, spp, depth, quantum=8, chunk=16, tail=8,
+                                       tail_chunk=3), sc)
+    c, _ = oracle.render(oracle.config(w, h, spp, depth, chunk=8), sc)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
+    seq, _ = oracle.render(oracle.config(w, h, spp, depth), sc)
+    one, _ = oracle.render(oracle.config(w, h, spp, depth, quantum=64), sc)
+    assert np.array_equal(seq.view(np.uint32), one.view(np.uint32))
+    # progressive frames restart the quanta at every frame
+    p, _ = oracle.render(oracle.config(w, h, 2 * spp, depth, quantum=16, frame_spp=spp), sc)
+    p0, _ = oracle.render(oracle.config(w, h, 2 * spp, depth, chunk=16, frame_spp=spp), sc)
+    assert np.array_equal(p.view(np.uint32), p0.view(np.uint32))
 
 
 def test_work_chunk_rejects_invalid_desc():

@@ -78,6 +78,7 @@ class vcrt_render_desc(ctypes.Structure):
         ("code_object_path", ctypes.c_char_p),
         ("accumulate_tail", ctypes.c_int32),
         ("accumulate_tail_chunk", ctypes.c_int32),
+        ("accumulate_quantum", ctypes.c_int32),
     ]
 
 
@@ -107,7 +108,7 @@ class vcrt_stats(ctypes.Structure):
         ("accumulate_tail", ctypes.c_int32),
         ("accumulate_tail_chunk", ctypes.c_int32),
         ("ring_entries", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("accumulate_quantum", ctypes.c_int32),
     ]
 
 
@@ -119,6 +120,7 @@ class vcrt_comm_id(ctypes.Structure):
 SIGNATURES = {
     "vcrt_default_desc": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_begin": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
+    "vcrt_work_quantum": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_work_chunk": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_work_tail": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc),
                                         ctypes.POINTER(ctypes.c_int32)]),

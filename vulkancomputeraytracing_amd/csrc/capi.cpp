@@ -89,6 +89,7 @@ struct RendererState {
     float4* d_cam_rec = nullptr;  // camera-relative records: big groups, sphere lists
     bool primary_lists = true;        // VCRT_PRIMARY_LISTS=0 turns them off
     // work decomposition
+    int32_t quantum = 1;  // the accumulation quantum G (a power of two)
     int32_t chunk = 1, nchunks = 1;
     int32_t tail_start = 0, tail_chunk = 1, tail_nchunks = 0;  // TraceParams' tail
     uint32_t total_pixels = 0, total_items = 0;
@@ -170,8 +171,26 @@ uint32_t tiles_for_rank(int32_t width, int32_t height, int32_t world, int32_t ra
     return static_cast<uint32_t>(n);
 }
 
-// Samples per work item for a desc: its accumulate_chunk (capped at spp), else the default for
-// the largest rank's share of the frame.
+// The accumulation quantum G (vcrt.h accumulate_quantum): the image depends on G alone. A
+// pixel's samples are summed in fp32 within each run of G consecutive samples, and the runs'
+// sums are quantized and added exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks of
+// them per pixel: 16, doubled while the frame's samples would need more. G does not depend on
+// the number of GPUs, so a sharded frame equals the one-GPU frame bit for bit with default descs
+// (round 4; before, the chunk was the quantum and followed the rank's share: K = 64 on one GPU,
+// 16 at N = 8, so the default images differed). Work items (chunks, the tail) hold whole quanta.
+constexpr int32_t kDefaultQuantum = 16;
+
+int32_t work_quantum(const vcrt_render_desc& d) {
+    if (d.accumulate_quantum > 0) return d.accumulate_quantum;
+    int32_t q = kDefaultQuantum;
+    while ((d.samples_per_pixel + q - 1) / q > vcrt::kAccumMaxChunks) q *= 2;
+    return q;
+}
+
+int32_t round_up(int32_t x, int32_t q) { return static_cast<int32_t>((int64_t{x} + q - 1) / q * q); }
+
+// Samples per work item for a desc: its accumulate_chunk, else the default for the largest rank's
+// share of the frame; rounded up to whole quanta and capped at spp.
 int32_t work_chunk(const vcrt_render_desc& d) {
     uint32_t max_tiles = 0;
     for (int32_t rr = 0; rr < d.world_size; rr++)
@@ -179,7 +198,7 @@ int32_t work_chunk(const vcrt_render_desc& d) {
     const int32_t k = d.accumulate_chunk > 0
                           ? d.accumulate_chunk
                           : default_chunk(64ull * max_tiles, d.samples_per_pixel);
-    return std::min(k, d.samples_per_pixel);
+    return std::min(round_up(k, work_quantum(d)), d.samples_per_pixel);
 }
 
 // The tail of the partition (vcrt.h vcrt_work_tail): the last T samples of every pixel in items
@@ -195,6 +214,7 @@ constexpr uint64_t kTailLaneItems = 6ull * 327680ull;
 
 int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk) {
     const int32_t spp = d.samples_per_pixel;
+    const int32_t q = work_quantum(d);
     *tail_chunk = 1;
     if (d.accumulate_tail < 0 || chunk >= spp) return 0;
     int32_t t = 0, kt = d.accumulate_tail_chunk;
@@ -209,20 +229,13 @@ int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk)
         t = 1 << static_cast<int>(std::lround(std::log2(raw)));  // nearest power of two
         if (4 * static_cast<int64_t>(t) > spp) return 0;
     }
-    const bool kt_rule = kt <= 0;
-    if (kt_rule) kt = std::max(4, chunk / 8);
-    kt = std::min(kt, t);
-    // A pixel takes at most kAccumMaxChunks chunks, head and tail together (vcrt_begin rejects
-    // more). The head alone fits (default_chunk keeps spp / K <= 512). When the tail does not
-    // fit beside it, a rule-made tail item grows until it does; a rule-made tail that cannot fit
-    // is dropped; explicit values stay as given (vcrt_begin then reports them).
-    const int32_t head = (spp - t + chunk - 1) / chunk;
-    const int32_t room = vcrt::kAccumMaxChunks - head;
-    if ((t + kt - 1) / kt > room) {
-        if (room > 0 && kt_rule) kt = (t + room - 1) / room;
-        else if (d.accumulate_tail == 0) return 0;
-    }
-    *tail_chunk = kt;
+    // whole quanta: the head ends on a quantum boundary (the tail grows to it), tail items are
+    // one quantum (the rule) or whole quanta, the last one ending at spp
+    const int32_t head_end = (spp - t) / q * q;
+    if (head_end <= 0) return 0;
+    t = spp - head_end;
+    kt = kt <= 0 ? q : round_up(kt, q);
+    *tail_chunk = std::min(kt, t);
     return t;
 }
 
@@ -231,8 +244,8 @@ void make_jitter(uint64_t base, int n, std::vector<float2>& out) {
     out.resize(static_cast<size_t>(n));
     for (int k = 0; k < n; k++) {
         const float i = static_cast<float>(base + k), i1 = static_cast<float>(base + k + 1);
-        out[k].x = -0.5f + vcrt::rand2(i, i);
-        out[k].y = -0.5f + vcrt::rand2(i1, i1);
+        out[k].x = vcrt::kJitterOffset + vcrt::rand2(i, i);  // shader.comp:48
+        out[k].y = vcrt::kJitterOffset + vcrt::rand2(i1, i1);
     }
 }
 
@@ -390,6 +403,8 @@ bool desc_valid(const vcrt_render_desc& d) {
     if (d.width > 65535 || d.height > 65535) return false;  // kernels pack y << 16 | x
     if (d.world_size <= 0 || d.rank < 0 || d.rank >= d.world_size) return false;
     if (d.blocks_per_cu < 0 || d.accumulate_chunk < 0) return false;
+    if (d.accumulate_quantum < 0 || (d.accumulate_quantum & (d.accumulate_quantum - 1)) != 0)
+        return false;  // a power of two (the kernel masks the sample index with G - 1)
     if (d.accumulate_tail < -1 || d.accumulate_tail_chunk < 0) return false;
     if (d.progressive != 0 && d.progressive != 1) return false;
     if (d.kernel_variant < VCRT_KERNEL_AUTO || d.kernel_variant > VCRT_KERNEL_CULL_FLAT) return false;
@@ -518,7 +533,7 @@ VkResult wait_gather() {
             return comm_state(g.comm) == vcrt::PollState::kFailed ? vcrt::PollState::kFailed
                                                                   : vcrt::PollState::kPending;
         },
-        vcrt::comm_timeout_ms());
+        vcrt::gather_timeout_ms(vcrt::comm_timeout_ms(), g.stats.kernel_ms + g.stats.resolve_ms));
     if (w == vcrt::WaitResult::kDone) return VK_SUCCESS;
     if (w == vcrt::WaitResult::kFailed && ev != hipSuccess && ev != hipErrorNotReady) {
         const VkResult r = to_vk(ev);  // the device itself failed
@@ -637,15 +652,14 @@ vcrt_result vcrt_default_desc(vcrt_render_desc* d) {
     if (!d) return VCRT_ERROR_INITIALIZATION_FAILED;
     std::memset(d, 0, sizeof(*d));
     d->struct_size = sizeof(vcrt_render_desc);
-    d->width = 1280;  // globals.glsl:16-17
-    d->height = 720;
-    d->samples_per_pixel = 1;  // globals.glsl:9-13 (#if 0 -> 1)
-    d->max_depth = 50;         // globals.glsl:14
-    const float from[3] = {13, 2, 3}, at[3] = {0, 0, 0}, up[3] = {0, 1, 0};
-    std::memcpy(d->camera.lookfrom, from, sizeof(from));
-    std::memcpy(d->camera.lookat, at, sizeof(at));
-    std::memcpy(d->camera.vup, up, sizeof(up));
-    d->camera.vfov = 20.0f;
+    d->width = vcrt::kRefImageWidth;  // globals.glsl:16-17
+    d->height = vcrt::kRefImageHeight;
+    d->samples_per_pixel = vcrt::kRefSamplesPerPixel;  // globals.glsl:9-13 (#if 0 -> 1)
+    d->max_depth = vcrt::kRefMaxRecursion;             // globals.glsl:14
+    std::memcpy(d->camera.lookfrom, vcrt::kRefLookfrom, sizeof(d->camera.lookfrom));  // :21-24
+    std::memcpy(d->camera.lookat, vcrt::kRefLookat, sizeof(d->camera.lookat));
+    std::memcpy(d->camera.vup, vcrt::kRefVup, sizeof(d->camera.vup));
+    d->camera.vfov = vcrt::kRefVfov;
     d->device = -1;
     d->rank = 0;
     d->world_size = 1;
@@ -656,6 +670,11 @@ vcrt_result vcrt_default_desc(vcrt_render_desc* d) {
 int32_t vcrt_work_chunk(const vcrt_render_desc* desc) {
     if (!desc || !desc_valid(*desc)) return VCRT_ERROR_INITIALIZATION_FAILED;
     return work_chunk(*desc);
+}
+
+int32_t vcrt_work_quantum(const vcrt_render_desc* desc) {
+    if (!desc || !desc_valid(*desc)) return VCRT_ERROR_INITIALIZATION_FAILED;
+    return work_quantum(*desc);
 }
 
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk) {
@@ -750,9 +769,12 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         if ((r = to_vk(hipMemset(g.d_fb_own, 0, own))) != VK_SUCCESS) return fail(r);
     }
     g.d_fb = g.d_fb_own;
-    // Work decomposition: (local tile, chunk of K samples) items; a pixel's chunk sums are
-    // combined exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks of them.
+    // Work decomposition: (local tile, chunk of K samples) items holding whole quanta; a pixel's
+    // quantum sums are combined exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks.
     g.total_pixels = g.local_tiles * 64u;  // local element slots incl. partial-tile padding
+    g.quantum = work_quantum(g.desc);
+    if ((spp + g.quantum - 1) / g.quantum > vcrt::kAccumMaxChunks)
+        return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
     g.chunk = work_chunk(g.desc);
     {
         const int32_t t = work_tail(g.desc, g.chunk, &g.tail_chunk);
@@ -760,9 +782,10 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         g.tail_nchunks = t > 0 ? (t + g.tail_chunk - 1) / g.tail_chunk : 0;
     }
     g.nchunks = (g.tail_start + g.chunk - 1) / g.chunk;
-    if (g.nchunks + g.tail_nchunks > vcrt::kAccumMaxChunks)
+    if (g.nchunks >= 0x10000 || g.tail_nchunks >= 0x10000)  // the kernel's 16-bit chunk field
         return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
-    g.direct = g.nchunks == 1 && g.tail_nchunks == 0 && !g.desc.progressive;
+    // one quantum covers the pixel: the lane divides its fp32 sum (the reference's arithmetic)
+    g.direct = g.quantum >= spp && !g.desc.progressive;
     {
         const uint64_t items = static_cast<uint64_t>(g.total_pixels) *
                                static_cast<uint64_t>(g.nchunks + g.tail_nchunks);
@@ -795,8 +818,12 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (const char* e = std::getenv("VCRT_ITEM_ORDER"))
         if (std::strcmp(e, "tile") == 0) g.work_flags &= ~vcrt::kFlagChunkMinor;
     if (const char* e = std::getenv("VCRT_ACCUM_RING")) {  // 0: off; n > 1: at most n entries
+        // (clamped to kRingMaxEntries: a lane keeps its entry + 1 in the top bits of its pixel
+        // index, so a larger ring would silently stop serving most pixels)
         g.accum_ring = std::atoi(e) != 0;
-        if (std::atoi(e) > 1) g.ring_max = static_cast<uint32_t>(std::atoi(e));
+        if (std::atoi(e) > 1)
+            g.ring_max = std::min<uint32_t>(static_cast<uint32_t>(std::atoi(e)),
+                                            vcrt::kRingMaxEntries);
     }
     if (g.debug_stats && (r = to_vk(hipMalloc(&g.d_debug, sizeof(g.stats.debug)))) != VK_SUCCESS)
         return fail(r);
@@ -808,6 +835,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         return fail(r);
     g.stats.local_tiles = static_cast<int32_t>(g.local_tiles);
     g.stats.accumulate_chunk = g.chunk;
+    g.stats.accumulate_quantum = g.quantum;
     g.stats.accumulate_tail = spp - g.tail_start;
     g.stats.accumulate_tail_chunk = g.tail_nchunks > 0 ? g.tail_chunk : 0;
     return VCRT_SUCCESS;
@@ -971,10 +999,10 @@ vcrt_result vcrt_draw_next_frame(void) {
     }
     const uint64_t spp_total =
         (g.desc.progressive ? g.accumulated : 0) + static_cast<uint64_t>(g.desc.samples_per_pixel);
-    // progressive frames add chunks to the pixels' exact sums: at most kAccumMaxChunks in all
+    // progressive frames add quanta to the pixels' exact sums: at most kAccumMaxChunks in all
     if (g.desc.progressive &&
         (g.accumulated / static_cast<uint64_t>(g.desc.samples_per_pixel) + 1) *
-                static_cast<uint64_t>(g.nchunks + g.tail_nchunks) >
+                static_cast<uint64_t>((g.desc.samples_per_pixel + g.quantum - 1) / g.quantum) >
             static_cast<uint64_t>(vcrt::kAccumMaxChunks))
         return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
     if (g.desc.progressive && g.accumulated > 0) {
@@ -1020,6 +1048,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.local_tiles = g.local_tiles;
         p.total_items = g.total_items;
         p.chunk = g.chunk;
+        p.quantum_mask = static_cast<uint32_t>(g.quantum - 1);
         p.nchunks = g.nchunks;
         p.tail_start = g.tail_start;
         p.tail_chunk = g.tail_chunk;
@@ -1130,6 +1159,8 @@ vcrt_result vcrt_draw_next_frame(void) {
                                  kc.f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
     }
     if (g.comm && g.desc.world_size > 1) {
+        // this rank's own render is complete (the stream synchronize above, no deadline); the
+        // exchange's deadline (wait_gather) scales with the frame time for the peers' renders
         VkResult r = gather_frame();
         if (r == VK_SUCCESS) r = wait_gather();
         if (r != VK_SUCCESS) return r;

@@ -33,9 +33,20 @@ inline int64_t comm_timeout_ms() {
     return 120000;
 }
 
+// Deadline of one frame's gather. The caller has waited for its own render (without a deadline)
+// before the gather starts, but rank 0's receive still covers its peers' renders, which finish
+// at about the same time in a balanced frame yet may lag by a fraction of a long one. So the
+// exchange gets the base deadline plus four times this rank's own frame time: a slow but alive
+// peer (a large spp, 4K, a stats build) is not mistaken for a lost one.
+inline int64_t gather_timeout_ms(int64_t base_ms, double frame_ms) {
+    const double extra = frame_ms > 0.0 ? 4.0 * frame_ms : 0.0;
+    return base_ms + static_cast<int64_t>(extra < 9.0e15 ? extra + 1.0 : 9.0e15);
+}
+
 // Polls `poll` (returns PollState) until it reports done or failed, or until `timeout_ms` have
 // passed since the call: kDone, kFailed or kTimedOut. The first polls run back to back (a gather
-// normally completes within a frame), then the wait backs off to sleeps of up to 1 ms. `now`
+// normally completes within a frame), then the wait backs off to sleeps of 20 us, and of 200 us
+// after ~20 ms (a frame waits at most that long past the gather's completion). `now`
 // returns milliseconds on a monotonic clock (injectable for tests).
 template <typename Poll, typename Now>
 WaitResult wait_with_deadline(Poll&& poll, int64_t timeout_ms, Now&& now) {
@@ -45,7 +56,7 @@ WaitResult wait_with_deadline(Poll&& poll, int64_t timeout_ms, Now&& now) {
         if (s == PollState::kDone) return WaitResult::kDone;
         if (s == PollState::kFailed) return WaitResult::kFailed;
         if (now() - start >= timeout_ms) return WaitResult::kTimedOut;
-        if (spin >= 64) std::this_thread::sleep_for(std::chrono::microseconds(spin < 1024 ? 20 : 1000));
+        if (spin >= 64) std::this_thread::sleep_for(std::chrono::microseconds(spin < 1024 ? 20 : 200));
     }
 }
 

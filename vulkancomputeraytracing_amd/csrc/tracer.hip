@@ -90,7 +90,7 @@ __device__ __forceinline__ Group load_group(const float4* lds, const TraceParams
 // (min_t, max_t), strict comparisons, max_t shrinks on acceptance.
 __device__ __forceinline__ void accept_root(float hb, float disc, float a, float& max_t, int& best,
                                             int j) {
-    const float min_t = 0.001f;
+    const float min_t = kMinT;
     const float sq = __builtin_sqrtf(disc);
     float root = (-hb - sq) / a;
     bool ok = true;
@@ -115,7 +115,7 @@ __device__ __forceinline__ void accept_root(float hb, float disc, float a, float
 // Outside the guarded ranges (tiny/huge/NaN values) it answers true and the exact path decides.
 __device__ __forceinline__ bool may_accept(float hb, float disc, float a, float max_t,
                                            bool ray_ok) {
-    const float min_t = 0.001f;
+    const float min_t = kMinT;
     const bool ok = ray_ok && disc >= 0x1p-100f && disc <= 0x1p100f && hb >= -0x1p60f &&
                     hb <= 0x1p60f;
     const float sq_hi = __uint_as_float(__float_as_uint(__builtin_amdgcn_sqrtf(disc)) + 4u);
@@ -243,7 +243,7 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
 __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
     const float sq = __builtin_sqrtf(disc);
     const float r1 = (-hb - sq) / a;
-    if (r1 > 0.001f) return r1;
+    if (r1 > kMinT) return r1;
     return (-hb + sq) / a;
 }
 
@@ -303,7 +303,7 @@ __device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a,
         sq = __builtin_sqrtf(disc);
     }
     const float r1 = div_a(-hb - sq, a, ya);
-    if (r1 > 0.001f) return r1;
+    if (r1 > kMinT) return r1;
     return div_a(-hb + sq, a, ya);
 #endif
 }
@@ -344,7 +344,7 @@ __device__ __forceinline__ void pair_disc_cam(const v2f dx, const v2f dy, const 
 }
 
 __device__ __forceinline__ void consider(float t, int idx, float& max_t, int& best) {
-    if (t > 0.001f && (t < max_t || (t == max_t && best >= 0 && idx < best))) {
+    if (t > kMinT && (t < max_t || (t == max_t && best >= 0 && idx < best))) {
         max_t = t;
         best = idx;
     }
@@ -690,6 +690,7 @@ __device__ __forceinline__ float hit_sign(float hb, float cc, float disc) {
 // (Round 2: the chunk level was wave-uniform -- every lane tested the nodes of every chunk some
 // lane needed, with per-lane min/max box tests on scalar-loaded boxes; as passes the nodes are
 // tested only for the lanes that need the chunk, by the near/far box test.)
+constexpr int kPendSky = -2;  // trace_impl's pend_best for a deferred sky segment
 constexpr int kChunkCap = 128;
 constexpr int kNodeCap = 576;
 constexpr int kGroupCap = 576;
@@ -905,7 +906,7 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         const float cc = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
         const float disc = hb * hb - a * cc;
         const float t = candidate_t_fast(hb, disc, a, ya);
-        if (act && t > 0.001f && t < 1e5f)
+        if (act && t > kMinT && t < kInfinity)
             atomicMin(&ws->key[e >> (F::kShift + 2)], pack_hit(t, tg.index(gi, s)));
     }
 }
@@ -1412,12 +1413,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     const bool chunk_minor = (P.flags & kFlagChunkMinor) != 0;
 
     bool done = false, need = true;
-    bool fin = false;  // the lane's chunk is finished and its sum in acc not yet added
+    bool fin = false;  // the lane's quantum is finished and its sum in acc not yet added
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
     // flat scan: a main-scan hit waits for the next iteration's shading (pend_t, pend_best;
     // pend_best < 0: none), which it shares with that iteration's camera rays
     float pend_t = 0.0f;
-    int pend_best = -1;
+    int pend_best = -1;  // -1: none; kPendSky: a sky segment
     int sample = 0, sample_end = 0, pass = 0;
     uint32_t q = 0;
     uint32_t pxy = 0;  // the item's pixel: y << 16 | x
@@ -1545,21 +1546,23 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             if (pass >= P.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
         } else {
             const float len = sqrt_fast(dot(d, d));  // length(d)
-            const float t = 0.5f * (d.y / len + 1.0f);
-            const float om = 1.0f - t;
-            contrib = mul(atten, mk(om + 0.5f * t, om + 0.7f * t, om + t));
+            contrib = mul(atten, sky_factor(d.y / len));
             ended = true;
         }
 
         if (ended) {
-            acc = add(acc, contrib);  // the chunk's fp32 sum in sample order
+            acc = add(acc, contrib);  // the quantum's fp32 sum in sample order
             ++sample;
             if (sample == sample_end) {
-                // the chunk is done: its sum in acc is retired at the top of the next iteration
-                // (few registers are live there: the accumulation code stays out of shading)
+                // the item is done: its last quantum's sum in acc is retired at the top of the
+                // next iteration (few registers are live there: the accumulation code stays out
+                // of shading)
                 fin = true;
                 need = true;
             } else {
+                // a quantum of G samples ends inside the item: its sum is retired the same way,
+                // and the item goes on with its next sample
+                if (((uint32_t)sample & P.quantum_mask) == 0u) fin = true;
                 const float2 jt = P.jitter[sample];
                 const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
                 o = cam;
@@ -1582,7 +1585,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             pargs = reinterpret_cast<const TraceParams*>(
                 (__attribute__((address_space(4))) const TraceParams*)(((uint64_t)hi << 32) | lo));
         }
-        if (fin) {  // ---- retire the finished chunk: its sum to the pixel ----
+        if (fin) {  // ---- retire the finished quantum: its sum to the pixel ----
             fin = false;
             if ((P.flags & kFlagDirect) != 0u) {
                 // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
@@ -1621,6 +1624,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 #endif
                 }
             }
+            acc = mk(0.f, 0.f, 0.f);  // the next quantum (of this item or the next) sums from 0
         }
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
@@ -1750,8 +1754,6 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         if (got) {
             q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
-            // shader.comp:43  pixel00 + x*delta_u + y*delta_v
-            acc = mk(0.f, 0.f, 0.f);
             const bool tail = g_chunk >= 0x10000u;
             const int k = tail ? P.tail_chunk : P.chunk;
             sample = (tail ? P.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
@@ -1792,7 +1794,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             const bool cam_now = fresh && (inf & 15u) != 15u && (P.flags & kFlagSceneBounded) != 0 &&
                                  aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
-            float mt = 1e5f;
+            float mt = kInfinity;
             int bst = -1;
             if (__ballot(cam_now)) {
                 if constexpr (kStats) {
@@ -1864,10 +1866,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             // One shading for the camera rays just traced and the main-scan hits of the last
             // iteration: the hit branches run once per iteration for both (a lane has at most
             // one of them; each lane's own sequence of operations is unchanged).
-            const bool pending = pend_best >= 0;
+            const bool pending = pend_best != -1;
             if (pending) {
                 mt = pend_t;
-                bst = pend_best;
+                bst = pend_best >= 0 ? pend_best : -1;  // kPendSky: the sky
                 pend_best = -1;
             }
             uint64_t t_cs = 0;
@@ -1883,7 +1885,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 
         // ---- one segment: scan the whole sphere list (functions.glsl:73-81) ----
         ++segs;
-        float max_t = 1e5f;
+        float max_t = kInfinity;
         int best = -1;
         uint32_t hit_groups = 0;
         if constexpr (kCull != 0) {
@@ -1932,9 +1934,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             pt.shade_hits += (uint64_t)__popcll(__ballot(best >= 0));
         }
         if constexpr (kFlat) {
-            if (best >= 0) {  // a hit: shaded with the next iteration's camera rays
+            // a hit is shaded with the next iteration's camera rays; so is the sky of a lane
+            // whose quantum ended in this iteration's camera phase (its sum in acc awaits the
+            // retire, so no second sample may end before it)
+            if (best >= 0 || fin) {
                 pend_t = max_t;
-                pend_best = best;
+                pend_best = best >= 0 ? best : kPendSky;
                 fresh = false;  // the ray is traced (it may have been a camera ray)
             } else {
                 fresh = shade_and_advance(max_t, best);  // the sky

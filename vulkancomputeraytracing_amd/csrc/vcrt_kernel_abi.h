@@ -78,6 +78,10 @@ struct TraceParams {
     // nchunks). No tail: tail_start = spp, tail_nchunks = 0.
     int32_t tail_start, tail_chunk, tail_nchunks;
     uint32_t blocks_head;
+    // the accumulation quantum G - 1 (G a power of two): a lane's fp32 sum is quantized and added
+    // to the pixel's sums at every sample index that is a multiple of G (vcrt_math.h
+    // "Accumulation"); items hold whole quanta
+    uint32_t quantum_mask;
     uint32_t flags;        // kFlag*
     float spp_total;       // kFlagDirect: the divisor (samples per pixel)
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
@@ -97,6 +101,10 @@ constexpr uint32_t kQueues = VCRT_QUEUES;
 constexpr uint32_t kMaxQueues = 32;        // counters the host allocates and zeroes
 constexpr uint32_t kRingMaxEntries = 63;  // entry + 1 in the top 6 bits of a lane's pixel index
 constexpr uint32_t kRingQBits = 26;
+// the kernel masks a queue index with kQueues - 1 and the host zeroes kMaxQueues counters
+static_assert((kQueues & (kQueues - 1u)) == 0u && kQueues >= 1u && kQueues <= kMaxQueues,
+              "VCRT_QUEUES: a power of two <= kMaxQueues");
+static_assert(kRingMaxEntries + 1u <= (1u << (32u - kRingQBits)), "ring entry field");
 
 constexpr int32_t kFlatMaxGroups = 1024;   // CULL_FLAT 16-bit entries: 10-bit group / node fields
 constexpr int32_t kFlatMaxGroups8 = 256;   // the LDS-table kernel: 8-bit fields, 16-bit candidates

@@ -23,6 +23,29 @@
 
 namespace vcrt {
 
+// ---------------------------------------------------------------------------------------
+// The reference's literals on the hot path, named once. Pinned against the reference files
+// themselves: tests/golden/make_constants_fixture.py parses them into
+// tests/golden/reference_constants.json, and tests/test_native_cpu.py checks these definitions,
+// the oracle's and vcrt_default_desc against it bit for bit (and that tracer.hip spells none
+// of them as a literal).
+constexpr float kRandDotX = 12.9898f;      // functions.glsl:11  dot(co, vec2(12.9898, 78.233))
+constexpr float kRandDotY = 78.233f;       // functions.glsl:11
+constexpr float kRandScale = 43758.5453f;  // functions.glsl:11  sin(...) * 43758.5453
+constexpr float kMinT = 0.001f;            // functions.glsl:76  global_hit_record.min_t
+constexpr float kInfinity = 1e5f;          // globals.glsl:26, functions.glsl:75: max_t per pass
+constexpr float kSkyHalf = 0.5f;           // functions.glsl:87  a = 0.5 * (unit_direction.y + 1.0)
+constexpr float kSkyOne = 1.0f;            // functions.glsl:87
+constexpr float kSkyBottom = 1.0f;         // functions.glsl:88  mix(vec3(1), vec3(.5,.7,1), a)
+constexpr float kSkyTopR = 0.5f, kSkyTopG = 0.7f, kSkyTopB = 1.0f;  // functions.glsl:88
+constexpr float kJitterOffset = -0.5f;     // shader.comp:48  (-0.5 + rand(vec2(i,i))) * du + ...
+// globals.glsl:9-24 (the `#if 0` resolved: SAMPLES_PER_PIXEL 1), the defaults of vcrt_default_desc
+constexpr int32_t kRefSamplesPerPixel = 1, kRefMaxRecursion = 50;
+constexpr int32_t kRefImageWidth = 1280, kRefImageHeight = 720;
+constexpr float kRefLookfrom[3] = {13.0f, 2.0f, 3.0f}, kRefLookat[3] = {0.0f, 0.0f, 0.0f},
+                kRefVup[3] = {0.0f, 1.0f, 0.0f};
+constexpr float kRefVfov = 20.0f;
+
 struct f3 {
     float x, y, z;
 };
@@ -284,22 +307,29 @@ __device__ __forceinline__ float sin_fast(float xf) {
 
 // functions.glsl:10-12  rand(co) = fract(sin(dot(co, vec2(12.9898,78.233))) * 43758.5453),
 // split as the sine's argument and the fract of the scaled sine
-VCRT_HD float rand_arg(float x, float y) { return x * 12.9898f + y * 78.233f; }
+VCRT_HD float rand_arg(float x, float y) { return x * kRandDotX + y * kRandDotY; }
 VCRT_HD float rand_of_sin(float s) {
-    const float p = s * 43758.5453f;
+    const float p = s * kRandScale;
     return p - __builtin_floorf(p);
 }
 
 VCRT_HD float rand2(float x, float y) {
     float arg = rand_arg(x, y);
-#ifdef VCRT_EXPERIMENT_FAST_SIN  // timing experiments only: not the canonical value
-    float p = __builtin_sinf(arg) * 43758.5453f;
-#elif defined(__HIP_DEVICE_COMPILE__)
-    float p = sin_fast(arg) * 43758.5453f;
+#if defined(__HIP_DEVICE_COMPILE__)
+    float p = sin_fast(arg) * kRandScale;
 #else
-    float p = sin_canonical(arg) * 43758.5453f;
+    float p = sin_canonical(arg) * kRandScale;
 #endif
     return p - __builtin_floorf(p);
+}
+
+// functions.glsl:85-88: the sky's factor mix(vec3(1), vec3(.5,.7,1), 0.5 * (y / |d| + 1)) for
+// the segment's direction d (not normalised first: y / length(d) is unit_direction.y)
+VCRT_HD f3 sky_factor(float y_over_len) {
+    const float t = kSkyHalf * (y_over_len + kSkyOne);
+    const float om = 1.0f - t;  // GLSL mix(x, y, a) = x * (1 - a) + y * a
+    return f3{kSkyBottom * om + kSkyTopR * t, kSkyBottom * om + kSkyTopG * t,
+              kSkyBottom * om + kSkyTopB * t};
 }
 
 // functions.glsl:58-62 with canonical pow(x,5): NaN for x < 0 (GLSL leaves it undefined)

@@ -32,11 +32,13 @@ class RenderDesc:
     world_size: int = 1             # shards: rank owns the 8x8 tiles with (tx + ty) % world == rank
     kernel_variant: int = N.KERNEL_AUTO
     blocks_per_cu: int = 0
-    accumulate_chunk: int = 0       # 0 = from the frame (work_chunk); >= spp: sequential order
+    accumulate_chunk: int = 0       # samples per work item: 0 = from the frame (work_chunk)
     progressive: bool = False       # frame f continues the sample sequence; average of all frames
     code_object_path: str | None = None
     accumulate_tail: int = 0        # tail samples per pixel: 0 = the rule (work_tail), -1 = none
     accumulate_tail_chunk: int = 0  # samples per tail item; 0 = the rule
+    accumulate_quantum: int = 0     # accumulation quantum G (the image depends on it alone):
+                                    # 0 = the rule (work_quantum); >= spp: sequential order
     _path_keepalive: bytes | None = field(default=None, repr=False)
 
     def to_c(self) -> N.vcrt_render_desc:
@@ -56,22 +58,30 @@ class RenderDesc:
         d.progressive = 1 if self.progressive else 0
         d.accumulate_tail = self.accumulate_tail
         d.accumulate_tail_chunk = self.accumulate_tail_chunk
+        d.accumulate_quantum = self.accumulate_quantum
         if self.code_object_path:
             self._path_keepalive = self.code_object_path.encode()
             d.code_object_path = self._path_keepalive
         return d
 
 
+def work_quantum(desc: RenderDesc) -> int:
+    """The accumulation quantum G the renderer uses for `desc`, from the C ABI
+    (vcrt_work_quantum: host only, no GPU): the oracle's `quantum` for the same image."""
+    return N.check_count("vcrt_work_quantum",
+                         N.lib().vcrt_work_quantum(ctypes.byref(desc.to_c())))
+
+
 def work_chunk(desc: RenderDesc) -> int:
-    """Samples per work item (the accumulation chunk) the renderer uses for `desc`, from the
-    C ABI (vcrt_work_chunk: host only, no GPU). The oracle's `chunk` for the same image."""
+    """Samples per work item of the head the renderer uses for `desc`, from the C ABI
+    (vcrt_work_chunk: host only, no GPU). A scheduling choice: the image depends on the
+    quantum (work_quantum) only."""
     return N.check_count("vcrt_work_chunk", N.lib().vcrt_work_chunk(ctypes.byref(desc.to_c())))
 
 
 def work_tail(desc: RenderDesc) -> tuple[int, int]:
     """(tail samples per pixel, samples per tail item) the renderer uses for `desc`, from the
-    C ABI (vcrt_work_tail: host only, no GPU); (0, 0) when there is no tail. With work_chunk,
-    the oracle's chunk partition for the same image."""
+    C ABI (vcrt_work_tail: host only, no GPU); (0, 0) when there is no tail."""
     kt = ctypes.c_int32(0)
     t = N.check_count("vcrt_work_tail", N.lib().vcrt_work_tail(ctypes.byref(desc.to_c()),
                                                                 ctypes.byref(kt)))
