@@ -782,3 +782,22 @@ def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth,
         assert st["ring_entries"] == 8
     else:
         assert st["ring_entries"] >= 8
+
+
+@pytest.mark.parametrize("stage", ["1", "0"])
+@pytest.mark.parametrize("scene,w,h,spp,depth", [("three", 96, 54, 40, 8),   # staged: 1 KB
+                                                  ("red", 33, 21, 1200, 3),  # too big: global
+                                                  ("final", 40, 24, 3, 10)])  # 485 spheres
+def test_smem_staged_tables_bitwise(oracle, monkeypatch, stage, scene, w, h, spp, depth):
+    """The SMEM scan's LDS copy of the shading rows and the jitter (TraceParams.stage_*, small
+    scenes: C2) gives the oracle's bits, as does the global-memory path (VCRT_STAGE_TABLES=0, or
+    tables beyond the staging budget)."""
+    monkeypatch.setenv("VCRT_STAGE_TABLES", stage)
+    got, st = gpu_render(scene, w, h, spp, depth, vc.KERNEL_SMEM)
+    assert st["kernel"] == "vcrt_trace_smem"
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
+                               oracle.scene(scene))
+    assert_bitwise(got, want, f"{scene} staged={stage}")
+    assert st["segments"] == segs
+    staged = stage == "1" and 48 * st["nspheres"] + 8 * spp <= 8192
+    assert (st["lds_bytes"] > 0) == staged

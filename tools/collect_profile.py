@@ -1,6 +1,9 @@
-"""Collect a gpurun profiling batch (tools/gpu_profile.sh) into profiles/<tag>_*:
-  <tag>_bench_{c4,c3,c2,c5}.json     the bench lines of the BASELINE configs
-  <tag>_bench_kernel_stats.csv       rocprofv3 --kernel-trace --stats of the c4 bench command
+"""Collect a gpurun profiling batch (tools/gpu_run.sh profile) into profiles/<tag>_*:
+  <tag>_bench_{c4,c3,c2,c5}.json     the bench lines of the BASELINE configs, their roofline
+                                     counters (traffic, VALU issue) merged from this batch's own
+                                     PMC passes (the same build and workload; bench.py merges
+                                     profiles/traffic.json the same way at run time)
+  <tag>_bench_kernel_stats[_cfg].csv rocprofv3 --kernel-trace --stats of each bench command
   <tag>_pmc_summary.json             the PMC passes per config and kernel, and derived figures
   traffic.json                       per workload key: the tracer kernel's HBM bytes per launch
                                      and VALU figures, read by bench.py when its kernel matches
@@ -29,8 +32,9 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
 dst = os.path.join(ROOT, "profiles")
 os.makedirs(dst, exist_ok=True)
 
-CFG_KEYS = {  # render_once arguments of the PMC passes (tools/gpu_profile.sh)
+CFG_KEYS = {  # render_once arguments of the PMC passes (tools/gpu_run.sh profile)
     "c4": ("final", 1920, 1080, 1024, 10),
+    "c3": ("final", 1920, 1080, 256, 10),
     "c2": ("three", 800, 450, 64, 8),
     "c5": ("stress4096", 3840, 2160, 4096, 50),
 }
@@ -60,12 +64,15 @@ def kernel_name(st):
 
 
 for cfg in ("c4", "c3", "c2", "c5"):
-    for ext in ("json", "err"):
-        p = os.path.join(src, f"bench_{cfg}.{ext}")
-        if os.path.exists(p):
-            shutil.copy(p, os.path.join(dst, f"{tag}_bench_{cfg}.{ext}"))
-shutil.copy(os.path.join(src, "kt", "bench_kernel_stats.csv"),
-            os.path.join(dst, f"{tag}_bench_kernel_stats.csv"))
+    p = os.path.join(src, f"bench_{cfg}.err")
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join(dst, f"{tag}_bench_{cfg}.err"))
+    kt = os.path.join(src, f"kt_{cfg}", "bench_kernel_stats.csv")
+    if os.path.exists(kt):
+        shutil.copy(kt, os.path.join(dst, f"{tag}_bench_kernel_stats"
+                                          f"{'' if cfg == 'c4' else '_' + cfg}.csv"))
+        shutil.copy(os.path.join(src, f"kt_{cfg}.json"),
+                    os.path.join(dst, f"{tag}_bench_under_rocprof_{cfg}.json"))
 
 summary = {}
 traffic_path = os.path.join(dst, "traffic.json")
@@ -100,6 +107,21 @@ for cfg, (scene, w, h, spp, depth) in CFG_KEYS.items():
     key = f"{scene}_{w}x{h}_s{spp}_d{depth}_n1"
     traffic[key] = dict(derived, source=f"profiles/{tag}_pmc_summary.json [{cfg}]",
                         round=tag)
+# the bench lines with this batch's counters (bench.py's own merge, redone with the fresh file)
+for cfg, (scene, w, h, spp, depth) in CFG_KEYS.items():
+    p = os.path.join(src, f"bench_{cfg}.json")
+    if not os.path.exists(p):
+        continue
+    line = json.loads([ln for ln in open(p) if ln.startswith("{")][-1])
+    prof = traffic.get(f"{scene}_{w}x{h}_s{spp}_d{depth}_n1", {})
+    if cfg in summary and prof.get("kernel") == line["roofline"]["kernel"]:
+        rf = line["roofline"]
+        rf["traffic"] = prof["hbm_bytes_per_launch"]
+        for k in ("valu_issue_frac", "valu_lane_util", "effective_clock_ghz"):
+            rf[k] = prof[k]
+        rf["profile"] = prof["source"]
+    with open(os.path.join(dst, f"{tag}_bench_{cfg}.json"), "w") as f:
+        f.write(json.dumps(line) + "\n")
 with open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w") as f:
     json.dump(summary, f, indent=1)
 with open(traffic_path, "w") as f:

@@ -1,0 +1,131 @@
+# The one GPU driver (run on the GPU box from the repo root, e.g.
+#   gpurun -- 'bash tools/gpu_run.sh test ab profile'):
+# every mode below runs in order; a failing step ends the call (nothing more touches the GPU).
+#
+#   test        pytest -m gpu (one process, per-test timeout) and smoke()
+#   bench       bench.py lines of the BASELINE configs in $CFGS (default c4 c3 c2 c5)
+#   ab          A/B timing, interleaved single-process renders (tools/ab.py): the current tree
+#               against the tree in $PREV (an earlier commit built by tools/mkab_tree.sh; any ABI)
+#               and the code objects / env settings in $OBJS (tools/ab.py syntax: OBJ@VAR=V,...),
+#               on $AB_CFGS (default c4; also c2, c3, stress) for $ROUNDS rounds; digests must agree
+#   sweep       the N-way shards of C4 rendered one after another (tools/shard_sweep.py), max and
+#               per-rank kernel ms for N in $WORLDS (default 2,4,8), $SWEEP_REPS times
+#   profile     the round's profile set for tools/collect_profile.py $TAG: bench lines (c4 c3 c2
+#               c5), rocprofv3 --kernel-trace --stats of each bench command, and PMC passes (one
+#               counter block per run: FETCH_SIZE, WRITE_SIZE, two SQ sets) of one frame of each
+#   phases      stats build (VCRT_DEBUG_STATS=1): s_memtime per phase of the flat scan ($RO args)
+#   wavetimes   diagnostics build $WT_OBJ (VCRT_DEBUG_STATS=2): wave lifetimes ($WT_ARGS)
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ROOT=${GRAFT_REPO_ROOT:-$PWD}
+OUT=$ROOT/gpurun_out
+
+cfg_args() {  # tools/ab.py / render_once.py arguments of a config
+  case $1 in
+    c2) echo "--scene three --width 800 --height 450 --spp 64 --depth 8";;
+    c3) echo "--spp 256";;
+    c4) echo "--spp 1024";;
+    c5) echo "--scene stress4096 --width 3840 --height 2160 --spp 4096 --depth 50";;
+    stress) echo "--scene stress4096 --width 3840 --height 2160 --spp 32 --depth 50";;
+  esac
+}
+
+bench_steps() {
+  case $1 in c5) echo "--steps 2 --warmup 1";; c2) echo "--steps 50 --warmup 5";;
+             *) echo "--steps 10 --warmup 3";; esac
+}
+
+mode_test() {
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; return 1; }
+  tail -1 $OUT/pytest_gpu.log
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
+    || { cat $OUT/smoke.log; return 1; }
+  tail -1 $OUT/smoke.log
+}
+
+mode_bench() {
+  for c in ${CFGS:-c4 c3 c2 c5}; do
+    timeout -k 10 300 python bench.py --config $c $(bench_steps $c) > $OUT/bench_$c.json \
+      2> $OUT/bench_$c.err || { tail -20 $OUT/bench_$c.err; return 1; }
+    python -c "import json,sys; d=json.load(open('$OUT/bench_$c.json')); print('$c', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+  done
+}
+
+ab_run() {  # tag, command...
+  local tag=$1; shift
+  timeout -k 10 200 "$@" > $OUT/abt.json 2>&1 || { cat $OUT/abt.json; return 1; }
+  echo "$tag $(grep -o '"msamples_per_s": [0-9.]*' $OUT/abt.json | head -1) $(grep -o '"kernel_ms": [0-9.]*' $OUT/abt.json | head -1) $(grep -o '"sha": "[0-9a-f]*"' $OUT/abt.json | head -1)"
+}
+
+mode_ab() {
+  for i in $(seq 1 ${ROUNDS:-2}); do
+    for c in ${AB_CFGS:-c4}; do
+      local a="$(cfg_args $c) --frames ${AB_FRAMES:-2}"
+      [ $c = c2 ] && a="$(cfg_args $c) --frames 20"
+      if [ -n "$PREV" ]; then
+        ab_run "prev $c" env VCRT_PKG_ROOT=$PREV python tools/ab.py default --rounds 1 $a || return 1
+      fi
+      ab_run "new $c" python tools/ab.py default --rounds 1 $a || return 1
+      for o in $OBJS; do ab_run "$o $c" python tools/ab.py $o --rounds 1 $a || return 1; done
+    done
+  done
+  echo ab_done
+}
+
+mode_sweep() {
+  for i in $(seq 1 ${SWEEP_REPS:-1}); do
+    timeout -k 10 300 python tools/shard_sweep.py --spp 1024 --worlds ${WORLDS:-2,4,8} \
+      > $OUT/sweep_$i.json 2> $OUT/sweep_$i.err || { tail -20 $OUT/sweep_$i.err; return 1; }
+    python - "$OUT/sweep_$i.json" <<'PY'
+import json, sys
+r = json.load(open(sys.argv[1]))
+for key in sorted(x for x in r if x.startswith("world")):
+    w = r[key]
+    print(f"full {r['full_ms']:.2f} ms {key}: max {w['max_ms']:.2f} sum {w['sum_ms']:.1f} "
+          f"estimate {w['ideal_efficiency']:.3f}")
+PY
+  done
+}
+
+mode_profile() {
+  local P=$OUT/prof
+  rm -rf $P && mkdir -p $P
+  for c in c4 c3 c2 c5; do
+    timeout -k 10 300 python bench.py --config $c $(bench_steps $c) > $P/bench_$c.json \
+      2> $P/bench_$c.err || { tail $P/bench_$c.err; return 1; }
+  done
+  for c in c4 c3 c2 c5; do
+    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt_$c \
+      -o bench -- python3 $ROOT/bench.py --config $c $(bench_steps $c) --no-cpu-baseline \
+      > $P/kt_$c.json 2> $P/kt_$c.err) || { tail $P/kt_$c.err; return 1; }
+  done
+  for c in c4 c3 c2 c5; do
+    local RO=$(cfg_args $c)
+    (cd /tmp &&
+     timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/${c}_fetch -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${c}_fetch.log 2>&1 &&
+     timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/${c}_write -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${c}_write.log 2>&1 &&
+     timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $P/${c}_sq1 -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${c}_sq1.log 2>&1 &&
+     timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_MUL_F32 --output-format csv -d $P/${c}_sq2 -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${c}_sq2.log 2>&1) \
+      || { echo "pmc $c failed"; return 1; }
+  done
+  echo profile_done
+}
+
+mode_phases() {
+  VCRT_DEBUG_STATS=1 timeout -k 10 200 python tools/render_once.py ${RO:---spp 64} \
+    --variant ${PV:-5} > $OUT/phases.json || return 1
+  python tools/phases_report.py $OUT/phases.json
+}
+
+mode_wavetimes() {
+  VCRT_DEBUG_STATS=2 timeout -k 10 120 python tools/wave_times.py ${WT_OBJ:-ab_objs/wt.hsaco} \
+    ${WT_ARGS:---spp 1024 --worlds 8} || return 1
+}
+
+for m in "$@"; do
+  echo "== $m"
+  mode_$m || { echo "mode $m failed"; exit 1; }
+done
+echo all_done

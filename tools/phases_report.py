@@ -1,12 +1,8 @@
-# Where the flat scan's wave time goes (VCRT_DEBUG_STATS=1: s_memtime per phase, stats kernel),
-# final scene 1080p 64 spp; variant $PV (default 5).
-set -o pipefail
-mkdir -p gpurun_out
-export TMPDIR=/tmp
-VCRT_DEBUG_STATS=1 timeout -k 10 200 python tools/render_once.py ${RO:---spp 64} --variant ${PV:-5} > gpurun_out/phases.json || exit 1
-python - <<'PY'
+"""Where the flat scan's wave time goes: the report of a stats-build frame (VCRT_DEBUG_STATS=1,
+s_memtime per phase; tools/gpu_run.sh phases)."""
 import json
-st = json.load(open("gpurun_out/phases.json"))
+import sys
+st = json.load(open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/phases.json"))
 d = st["debug"]
 wi = d[0]
 tot = d[14]
@@ -30,4 +26,3 @@ if len(d) > 31 and d[24]:
 if len(d) > 22 and d[22]:
     print("flat passes per wave-iter %.2f, partial %.2f; entries per live lane %.3f" % (
         d[22] / wi, d[21] / wi, d[19] / d[20]))
-PY

@@ -36,6 +36,8 @@ using vcrt::to_vk;
 
 // segments (u64 at 8), work_done[2] (u64 at 16), then the work-queue counters from 256
 constexpr size_t kCounterBytes = 256 + vcrt::kMaxQueues * 4 * vcrt::kQueueStride;
+// LDS for the SMEM scan's staged tables (a few spheres' shading rows and the jitter table)
+constexpr uint32_t kStageMaxBytes = 8192;
 constexpr int32_t kDefaultChunk = 64;        // samples per work item (upper end)
 
 struct RendererState {
@@ -60,6 +62,7 @@ struct RendererState {
     // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global, 3 = boxes in LDS (flat scan)
     int cull_lane_tables = 0;
     bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
+    bool stage_tables = true;    // VCRT_STAGE_TABLES=0: the SMEM scan reads its tables globally
     uint32_t ring_max = vcrt::kRingMaxEntries;
     uint32_t lds_per_cu = 0;     // LDS bytes per CU (160 KB on gfx950)
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
@@ -817,6 +820,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     g.work_flags |= vcrt::kFlagChunkMinor;
     if (const char* e = std::getenv("VCRT_ITEM_ORDER"))
         if (std::strcmp(e, "tile") == 0) g.work_flags &= ~vcrt::kFlagChunkMinor;
+    if (const char* e = std::getenv("VCRT_STAGE_TABLES")) g.stage_tables = std::atoi(e) != 0;
     if (const char* e = std::getenv("VCRT_ACCUM_RING")) {  // 0: off; n > 1: at most n entries
         // (clamped to kRingMaxEntries: a lane keeps its entry + 1 in the top bits of its pixel
         // index, so a larger ring would silently stop serving most pixels)
@@ -1062,7 +1066,21 @@ vcrt_result vcrt_draw_next_frame(void) {
         for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
         const KernelChoice kc = select_kernel();
         hipFunction_t f = g.debug_stats == 1 ? kc.stats : kc.f;
-        const uint32_t block = kc.block, lds = kc.lds;
+        const uint32_t block = kc.block;
+        uint32_t lds = kc.lds;
+        // the linear SMEM scan of a small scene stages its shading and jitter tables in LDS
+        // (TraceParams.stage_*): C2 (4 spheres, 64 spp) is latency-bound on those reads
+        p.stage_spheres = 0u;
+        p.stage_spp = 0u;
+        if (kc.f == g.k_trace_smem && g.nspheres > 0 && g.stage_tables) {
+            const uint32_t bytes = 48u * static_cast<uint32_t>(g.nspheres) +
+                                   8u * static_cast<uint32_t>(g.desc.samples_per_pixel);
+            if (bytes <= kStageMaxBytes) {
+                p.stage_spheres = static_cast<uint32_t>(g.nspheres);
+                p.stage_spp = static_cast<uint32_t>(g.desc.samples_per_pixel);
+                lds = (bytes + 15u) & ~15u;
+            }
+        }
         const int variant = kc.variant;
         // the stage names the entry point this draw dispatches (Shader.cpp:89 names "main")
         g.stage.pName = kc.name;

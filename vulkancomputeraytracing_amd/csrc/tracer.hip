@@ -232,12 +232,6 @@ __device__ __forceinline__ void scan_spheres(const TraceParams& p, const float4*
 //      rules a box out when its whole stretch of the line lies behind -tau as well.
 //      (tau = sqrt(3.2e-7 Q / a), 7% above 5.02u Q / a for the roundings of Q, 1/a and sqrt.)
 // Waves holding a ray outside the guarded range scan the original table in reference order.
-#ifndef VCRT_LEVELS_NF
-#define VCRT_LEVELS_NF 1  // the LDS-table kernel's node level by near/far planes from LDS (0: scalar min/max)
-#endif
-#ifndef VCRT_BOX_CLIP
-#define VCRT_BOX_CLIP 1  // (4): 0 = the line test alone (A/B builds)
-#endif
 
 // t of one candidate as hit_sphere would accept it (finite case, fact (1)).
 __device__ __forceinline__ float candidate_t(float hb, float disc, float a) {
@@ -294,9 +288,6 @@ __device__ __forceinline__ float sqrt_fast(float x) {
 }
 
 __device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a, float ya) {
-#ifdef VCRT_EXACT_CANDIDATE_OPS  // A/B builds: hipcc's full sequences
-    return candidate_t(hb, disc, a);
-#else
     float sq = sqrt_unscaled(disc);
     if (disc < 0x1p-96f) {
         asm volatile("");  // a real branch: hipcc would otherwise run the full sqrt for every lane
@@ -305,7 +296,6 @@ __device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a,
     const float r1 = div_a(-hb - sq, a, ya);
     if (r1 > kMinT) return r1;
     return div_a(-hb + sq, a, ya);
-#endif
 }
 
 // A member whose origin lies outside or on it (cc >= 0) while the ray points away from its
@@ -387,7 +377,7 @@ __device__ __forceinline__ BoxRay box_ray(const TraceParams& p, const f3 o, cons
     BoxRay r;
     const float on = __builtin_amdgcn_sqrtf(dot(o, o)) + p.box_margin[0];
     const float Q = on * on + p.box_margin[1];
-    const float tau = VCRT_BOX_CLIP ? __builtin_amdgcn_sqrtf(3.2e-7f * Q * ya) : 0.0f;
+    const float tau = __builtin_amdgcn_sqrtf(3.2e-7f * Q * ya);  // (4)
     const float ax = box_axis(o.x, d.x, tau, r.ix, r.cx), ay = box_axis(o.y, d.y, tau, r.iy, r.cy),
                 az = box_axis(o.z, d.z, tau, r.iz, r.cz);
     const float J = 2.002f * fmaxf(fmaxf(ax, ay), az);  // 1.001 J
@@ -414,10 +404,9 @@ __device__ __forceinline__ v2f box_gap(const BoxRay& r, float4 b0, float4 b1, fl
     tn.y = fmaxf(fmaxf(fminf(tlx.y, thx.y), fminf(tly.y, thy.y)), fminf(tlz.y, thz.y));
     tf.x = fminf(fminf(fmaxf(tlx.x, thx.x), fmaxf(tly.x, thy.x)), fmaxf(tlz.x, thz.x));
     tf.y = fminf(fminf(fmaxf(tlx.y, thx.y), fmaxf(tly.y, thy.y)), fmaxf(tlz.y, thz.y));
-    if (VCRT_BOX_CLIP) {  // (4): the stretch of the line behind -tau does not count
-        tn.x = fmaxf(tn.x, 0.0f);
-        tn.y = fmaxf(tn.y, 0.0f);
-    }
+    // (4): the stretch of the line behind -tau does not count
+    tn.x = fmaxf(tn.x, 0.0f);
+    tn.y = fmaxf(tn.y, 0.0f);
     return vfma(K, r.c2, (tf - tn) + r.c1);
 }
 
@@ -654,10 +643,8 @@ __device__ __forceinline__ uint32_t push_bound_pair_nf(uint32_t acc, const BoxRa
     tn.y = fmaxf(fmaxf(tnx.y, tny.y), tnz.y);
     tf.x = fminf(fminf(tfx.x, tfy.x), tfz.x);
     tf.y = fminf(fminf(tfx.y, tfy.y), tfz.y);
-    if (VCRT_BOX_CLIP) {  // (4), as box_gap
-        tn.x = fmaxf(tn.x, 0.0f);
-        tn.y = fmaxf(tn.y, 0.0f);
-    }
+    tn.x = fmaxf(tn.x, 0.0f);  // (4), as box_gap
+    tn.y = fmaxf(tn.y, 0.0f);
     const v2f D = vfma(ld2(a.k + off), r.c2, (tf - tn) + r.c1);
     return push_sign(push_sign(acc, D.y), D.x);
 }
@@ -1087,7 +1074,6 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             // chunk, per-lane bits -> node entries
             const int nn = min(8, (ncg - base) >> 3);
             uint32_t out = 0;
-#if VCRT_LEVELS_NF
             {  // near/far planes from the LDS copy of the chunk's node boxes, by the ray's signs
                 const NearFarAddr na = near_far_addr(tnode + kNS * ((uint32_t)base >> 6),
                                                      br.ix.x, br.iy.x, br.iz.x);
@@ -1095,15 +1081,6 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                 for (int k = 3; k >= 0; k--) out = push_bound_pair_nf(out, br, na, 80 * k);
                 out &= (1u << nn) - 1u;
             }
-#else
-            cfloat4* nb = node + 4 * (base >> 4);
-            BoundPair cur = load_bound_pair(nb + 4 * ((nn - 2) >> 1));
-            for (int j = nn - 2; j >= 0; j -= 2) {
-                const BoundPair nxt = load_bound_pair(nb + 4 * ((j >= 2 ? j - 2 : j) >> 1));
-                out = push_bound_pair(out, br, cur.b0, cur.b1, cur.b2, cur.b3);
-                cur = nxt;
-            }
-#endif
             n_bounds += (uint32_t)nn;
             uint32_t nodes = in_chunk ? ~out & ((1u << nn) - 1u) : 0u;
             if constexpr (kStats) {
@@ -1306,6 +1283,34 @@ __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, ui
     return px;
 }
 
+// The jitter of sample i (shader.comp:48) and a hit sphere's shading rows, from the LDS copy the
+// SMEM scan stages for small scenes (TraceParams.stage_*), else from global memory.
+template <bool kStageable>
+__device__ __forceinline__ float2 jitter_at(const TraceParams& p, const float4* lds, int i) {
+    if constexpr (kStageable) {
+        if (p.stage_spp != 0u)
+            return reinterpret_cast<const float2*>(lds + 3u * p.stage_spheres)[i];
+    }
+    return p.jitter[i];
+}
+
+template <bool kStageable>
+__device__ __forceinline__ void shading_rows(const TraceParams& p, const float4* lds, int best,
+                                             float4& cr, float4& sh, float4& mat) {
+    if constexpr (kStageable) {
+        if (p.stage_spp != 0u) {
+            const uint32_t ns = p.stage_spheres;
+            cr = lds[best];
+            sh = lds[ns + best];
+            mat = lds[2u * ns + best];
+            return;
+        }
+    }
+    cr = p.center_radius[best];
+    sh = p.shade[best];
+    mat = p.material[best];
+}
+
 // kCull: 0 = linear scan (kLds: table in LDS), 1 = culled scan, 2 = per-lane culled scan
 // with the group tables copied to LDS, 3 = per-lane culled scan on global tables.
 template <bool kLds, bool kStats, int kCull = 0>
@@ -1327,6 +1332,23 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         for (int i = threadIdx.x; i < nq; i += blockDim.x) lds_geom[i] = P.geom[i];
         __syncthreads();
     }
+    // The SMEM scan of a small scene reads the shading rows and the jitter from an LDS copy
+    // (TraceParams.stage_*: [stage_spheres] center_radius, shade, material, then the jitter).
+    constexpr bool kStageable = kCull == 0 && !kLds;
+    if constexpr (kStageable) {
+        if (P.stage_spp != 0u) {
+            const uint32_t ns = P.stage_spheres;
+            for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
+                lds_dyn[i] = P.center_radius[i];
+                lds_dyn[ns + i] = P.shade[i];
+                lds_dyn[2u * ns + i] = P.material[i];
+            }
+            float2* jd = reinterpret_cast<float2*>(lds_dyn + 3u * ns);
+            for (uint32_t i = threadIdx.x; i < P.stage_spp; i += blockDim.x) jd[i] = P.jitter[i];
+            __syncthreads();
+        }
+    }
+
     // group-pair boxes: the flat scan reads the near/far layout (80 B per pair), the others
     // the pair-SoA one (64 B)
     constexpr bool kFlat = kCull == 4 || kCull == 5 || kCull == 6;
@@ -1358,13 +1380,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     }
     if constexpr (kCull == 4) {  // LDS: near/far boxes, 80-B group records with uint16 indices
         const int nb = (P.ncgroups >> 3) * kNS, ng = P.ncgroups * 5;
-#if VCRT_LEVELS_NF
         {  // and the chunks' node boxes (near/far, padded records) after the group records
             const int nn = ((P.ncgroups + 63) >> 6) * kNS;
             for (int i = threadIdx.x; i < nn; i += blockDim.x)
                 if (i % kNS != 20u) lds_geom[nb + ng + i] = tnode[i - i / kNS];
         }
-#endif
         for (int i = threadIdx.x; i < nb; i += blockDim.x)
             if (i % kNS != 20u) lds_geom[i] = tbound[i - i / kNS];
         for (int i = threadIdx.x; i < ng; i += blockDim.x) {
@@ -1381,13 +1401,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         __syncthreads();
         tbound = lds_geom;
         tg.geom = lds_geom + nb;
-#if VCRT_LEVELS_NF
         tnode = lds_geom + nb + ng;
         ws = reinterpret_cast<WS*>(lds_geom + nb + ng + ((P.ncgroups + 63) >> 6) * kNS) +
              (threadIdx.x >> 6);
-#else
-        ws = reinterpret_cast<WS*>(lds_geom + nb + ng) + (threadIdx.x >> 6);
-#endif
         static_assert(kNS == 21u && sizeof(WS) == kWaveScratchBytes8,
                       "host LDS size (capi.cpp select_kernel)");
     }
@@ -1444,15 +1460,6 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     const uint32_t total_blocks = P.total_items >> 6;
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
     uint32_t q_x = blockIdx.x & (kQueues - 1u), q_drained = 0u;  // the wave's queue; found empty
-#ifdef VCRT_STATIC_FIRST  // experiment: each wave's first block of its queue without an atomic
-    // (the queue's k-th wave takes its k-th block; the counter then counts past those)
-    const uint32_t q_wpg = blockDim.x >> 6;
-    uint32_t q_first = (blockIdx.x / kQueues) * q_wpg + (threadIdx.x >> 6);
-#endif
-#ifdef VCRT_PAIR_FETCH
-    uint32_t q_pend = ~0u;
-    bool q_pair = true;
-#endif
     uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
     bool blk_tail = false;
     // the wave's accumulation ring (see RingEntry): next entry to hand out; the current block's
@@ -1478,9 +1485,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         bool ended = false, fresh_cam = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
         if (best >= 0) {
-            const float4 cr = P.center_radius[best];
-            const float4 sh = P.shade[best];
-            const float4 mat = P.material[best];
+            float4 cr, sh, mat;
+            shading_rows<kStageable>(P, lds_dyn, best, cr, sh, mat);
             const f3 point = add(scale(max_t, d), o);
             // normal = (point - centre) / radius: the unscaled division with one reciprocal
             // (exact: candidate_t_fast's argument) for numerators and radius in [2^-40, 2^30]
@@ -1563,7 +1569,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // a quantum of G samples ends inside the item: its sum is retired the same way,
                 // and the item goes on with its next sample
                 if (((uint32_t)sample & P.quantum_mask) == 0u) fin = true;
-                const float2 jt = P.jitter[sample];
+                const float2 jt = jitter_at<kStageable>(P, lds_dyn, sample);
                 const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
                 o = cam;
                 d = sub(ps, cam);
@@ -1597,13 +1603,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // the chunk sum, quantized: RN_even(S * 2^32) (an integer below 2^44), summed
                 // exactly over the pixel's chunks in double; |S| >= 2^12, inf or NaN make the
                 // pixel NaN (vcrt_math.h "Accumulation")
-                const float amax = fmaxf(fmaxf(fabsf(acc.x), fabsf(acc.y)), fabsf(acc.z));
-                const bool ok = amax < kAccumLimit && acc.x == acc.x && acc.y == acc.y &&
-                                acc.z == acc.z;
-                const double nan = __builtin_nan("");
-                const double v0 = ok ? (double)__builtin_rintf(acc.x * kAccumScale) : nan;
-                const double v1 = ok ? (double)__builtin_rintf(acc.y * kAccumScale) : nan;
-                const double v2 = ok ? (double)__builtin_rintf(acc.z * kAccumScale) : nan;
+                // (three compares with |.| modifiers: NaN compares false; the NaN case in a real
+                // branch, so the common path converts without selects)
+                float ax = acc.x, ay = acc.y, az = acc.z;
+                if (!(fabsf(ax) < kAccumLimit && fabsf(ay) < kAccumLimit &&
+                      fabsf(az) < kAccumLimit)) {
+                    asm volatile("");
+                    ax = ay = az = __builtin_nanf("");
+                }
+                const double v0 = (double)__builtin_rintf(ax * kAccumScale);
+                const double v1 = (double)__builtin_rintf(ay * kAccumScale);
+                const double v2 = (double)__builtin_rintf(az * kAccumScale);
                 const uint32_t qi = q & kQMask, ent = q >> kRingQBits;
                 // the pixel's ring entry while it still holds this pixel (LDS atomics), else
                 // global memory (two branches: a pointer that may be either would make flat
@@ -1615,13 +1625,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     atomicAdd(s + 2, v2);
                 } else {
                     double* s = P.accum + 4u * qi;
-#ifdef VCRT_EXPERIMENT_NO_ATOMICS  // timing experiments only: wrong image
-                    if (acc.x == 12345.0f) s[0] = v0;
-#else
                     atomicAdd(s + 0, v0);
                     atomicAdd(s + 1, v1);
                     atomicAdd(s + 2, v2);
-#endif
                 }
             }
             acc = mk(0.f, 0.f, 0.f);  // the next quantum (of this item or the next) sums from 0
@@ -1643,46 +1649,19 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // counter; a wave whose queue is drained moves on to the next one, and is done
                 // when it has found every queue drained
                 uint32_t b = ~0u;
-#ifdef VCRT_STATIC_FIRST
-                if (q_first != ~0u) {
-                    if (q_first < (total_blocks + kQueues - 1u - q_x) / kQueues)
-                        b = kQueues * q_first + q_x;
-                    q_first = ~0u;
-                }
-#endif
-#ifdef VCRT_PAIR_FETCH  // experiment: two blocks per fetch while the queue is < 3/4 handed out
-                if (q_pend != ~0u) {
-                    b = q_pend;
-                    q_pend = ~0u;
-                }
-#endif
                 while (b == ~0u && q_drained < kQueues) {
                     const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
                     const uint32_t nq = (total_blocks + kQueues - 1u - q_x) / kQueues;
                     uint32_t k = 0;
-#ifdef VCRT_PAIR_FETCH
-                    const uint32_t amt = q_pair ? 2u : 1u;
-#else
                     const uint32_t amt = 1u;
-#endif
                     if ((int)lane == leader) k = atomicAdd(P.work + kQueueStride * q_x, amt);
                     k = __builtin_amdgcn_readfirstlane(__shfl(k, leader));
-#ifdef VCRT_STATIC_FIRST
-                    k += ((gridDim.x + kQueues - 1u - q_x) / kQueues) * q_wpg;  // q_x's static
-#endif
                     if (k < nq) {
                         b = kQueues * k + q_x;
-#ifdef VCRT_PAIR_FETCH
-                        if (amt == 2u && k + 1u < nq) q_pend = b + kQueues;
-                        q_pair = 4u * k < 3u * nq;
-#endif
                         break;
                     }
                     ++q_drained;
                     q_x = (q_x + 1u) & (kQueues - 1u);
-#ifdef VCRT_PAIR_FETCH
-                    q_pair = false;
-#endif
                 }
                 if (b == ~0u) {  // queues drained: lanes still wanting work are done
 #ifdef VCRT_WAVE_END_TIMES
@@ -1759,7 +1738,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             sample = (tail ? P.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
             sample_end = min(sample + k, tail ? P.spp : P.tail_start);
             // first camera ray of the chunk, shader.comp:48-52
-            const float2 jt = P.jitter[sample];
+            const float2 jt = jitter_at<kStageable>(P, lds_dyn, sample);
             const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
             o = cam;
             d = sub(ps, cam);

@@ -89,6 +89,11 @@ struct TraceParams {
     // per wave (0: none; <= kRingMaxEntries) at byte ring_off of the dynamic LDS, wave w of the
     // workgroup at ring_off + 32 ring_n w. Needs local pixels < 2^kRingQBits.
     uint32_t ring_off, ring_n;
+    // The linear SMEM scan's staging (small scenes, C2): when stage_spp != 0 the kernel copies
+    // the shading tables of the stage_spheres spheres (center_radius, shade, material: 48 B each)
+    // and the jitter table (stage_spp float2) to the start of the dynamic LDS and reads them
+    // there: the per-hit and per-sample reads leave global memory (L2 latency on every bounce).
+    uint32_t stage_spheres, stage_spp;
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)

@@ -268,10 +268,6 @@ __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
     const uint32_t below = (uint32_t)sb & 0x1FFFFFFFu;
     const bool ok = __builtin_fabsf(xf) < 0x1p19f && __builtin_fabs(r) >= 0x1p-12 &&
                     below - (0x10000000u - 0x200u) > 0x400u;
-#if VCRT_SINSB
-    __builtin_amdgcn_sched_barrier(0);  // one evaluation at a time: the three rand() calls of a
-                                        // diffuse hit interleaved would spill VGPRs
-#endif
     return ok;
 }
 
@@ -280,12 +276,6 @@ __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
 // canonically in one loop (one inlined copy of the fdlibm path instead of three).
 __device__ __forceinline__ void sin3(float a1, float a2, float a3, float& s1, float& s2,
                                      float& s3) {
-#ifdef VCRT_EXPERIMENT_FAST_SIN  // timing experiments only: not the canonical value
-    s1 = __builtin_amdgcn_sinf(a1 * 0.15915494f);
-    s2 = __builtin_amdgcn_sinf(a2 * 0.15915494f);
-    s3 = __builtin_amdgcn_sinf(a3 * 0.15915494f);
-    return;
-#endif
     const bool ok1 = sin_fast_try(a1, s1), ok2 = sin_fast_try(a2, s2), ok3 = sin_fast_try(a3, s3);
     if (!(ok1 && ok2 && ok3)) {
 #pragma nounroll
