@@ -111,7 +111,7 @@ typedef struct vcrt_render_desc {
     int32_t accumulate_tail_chunk; /* samples per tail item; 0 = the rule. Tail and tail items
                                       are rounded to multiples of the quantum. */
     int32_t accumulate_quantum; /* the accumulation quantum G (a power of two; 0 = the rule,
-                                   vcrt_work_quantum: 16, doubled while a pixel would take more
+                                   vcrt_work_quantum: 4, doubled while a pixel would take more
                                    than 512 quanta). A pixel's samples are summed in fp32 in sample
                                    order within each quantum of G consecutive samples (restarting
                                    at every progressive frame); when one quantum covers the pixel
@@ -176,9 +176,9 @@ int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
 /* Tail samples per pixel that vcrt_begin(desc) uses (0: none) and, in *tail_chunk, the samples
  * per tail item; host only. The rule: about six head items per lane of the persistent grid,
  * T = 6 * chunk * 327680 / (64 * the largest rank's tiles) rounded to a power of two, in items
- * of one quantum; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel. The head
- * ends on a quantum boundary (T is adjusted) and tail items are whole quanta. Negative VkResult
- * for an invalid desc. */
+ * of max(4, chunk / 8) samples; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel.
+ * The head ends on a quantum boundary (T is adjusted) and tail items are rounded up to whole
+ * quanta. Negative VkResult for an invalid desc. */
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
  * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final

@@ -112,7 +112,7 @@ def test_c4_sharded_eight_ways_equals_one_gpu(oracle):
     world = 8
     d1 = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp)
     d8 = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
-    assert vc.renderer.work_quantum(d1) == vc.renderer.work_quantum(d8) == 16
+    assert vc.renderer.work_quantum(d1) == vc.renderer.work_quantum(d8) == 4
     assert vc.renderer.work_chunk(d1) != vc.renderer.work_chunk(d8)  # 64 against 16
     full, st1 = render_full("c4")  # the default 1-GPU frame
     pad = D.tiles_per_rank(w, h, world)

@@ -100,7 +100,7 @@ def test_bitwise_vs_oracle(oracle, scene, w, h, spp, depth, variant):
 @pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("scene,w,h,spp,depth,chunk,quantum", [
     ("final", 64, 36, 64, 10, 16, 0),   # 4 items of one quantum (16)
-    ("final", 48, 30, 40, 10, 0, 0),    # the default for a tiny frame: quanta 16 + 16 + 8
+    ("final", 48, 30, 40, 10, 0, 0),    # the default for a tiny frame: ten quanta of 4
     ("three", 72, 40, 96, 8, 7, 1),     # 14 items (the last of 5), every sample a quantum
     ("final", 64, 36, 48, 10, 32, 4),   # items of 8 quanta (the last of 4): mid-item retires
     ("three", 40, 24, 40, 8, 0, 8),     # 5 quanta of 8 inside items of 32 and 8
@@ -605,7 +605,7 @@ def test_bench_multirank_gather_bitwise():
     assert res["n_gpus"] == 3
     assert res["validated"]["bitwise_vs_1gpu"] is True
     assert res["validated"]["bitwise_vs_oracle"] is True
-    assert res["validated"]["quantum"] == [16, 16]
+    assert res["validated"]["quantum"] == [4, 4]
     pr = res["per_rank_kernel_ms"]
     assert len(pr["ranks"]) == 3 and 0 < pr["min"] <= pr["max"]
     assert "gather_ms" in res

@@ -285,7 +285,7 @@ def test_srgb8_thresholds_agree_with_oracle(oracle):
 
 
 def _quantum_rule(spp):
-    q = 16
+    q = 4
     while -(-spp // q) > 512:
         q *= 2
     return q
@@ -293,7 +293,7 @@ def _quantum_rule(spp):
 
 @pytest.mark.parametrize("spp", [1, 3, 16, 64, 256, 1024, 4096, 8192, 8193, 100000])
 def test_work_quantum_rule(spp):
-    """vcrt_work_quantum (the accumulation quantum G; host only): 16, doubled while a pixel would
+    """vcrt_work_quantum (the accumulation quantum G; host only): 4, doubled while a pixel would
     take more than 512 quanta -- the same for every world size and rank (so the default image
     does not depend on the number of GPUs); an explicit power of two is taken as given, anything
     else is an invalid desc."""
@@ -377,7 +377,7 @@ def test_work_tail_rule(w, h, spp):
             head_end = (spp - want) // q * q
             want = spp - head_end if head_end > 0 else 0
         assert t == want
-        assert kt == (min(q, want) if want else 0)
+        assert kt == (min(_round_up(max(4, k // 8), q), want) if want else 0)
         if t:
             assert (spp - t) % q == 0
         d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world,
@@ -389,8 +389,8 @@ def test_work_tail_rule(w, h, spp):
         d.accumulate_tail = -1
         assert vc.renderer.work_tail(d) == (0, 0)
     if (w, h, spp) == (1920, 1080, 1024):  # the bench config on 1/2/4/8 GPUs
-        for world, want in ((1, (64, 64, 16)), (2, (64, 128, 16)), (4, (32, 128, 16)),
-                            (8, (16, 128, 16))):
+        for world, want in ((1, (64, 64, 8)), (2, (64, 128, 8)), (4, (32, 128, 4)),
+                            (8, (16, 128, 4))):
             d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
             assert (vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d) == want
 

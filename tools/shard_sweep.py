@@ -19,10 +19,12 @@ p.add_argument("--variant", type=int, default=0)
 p.add_argument("--code-object", default=None)
 p.add_argument("--tail", type=int, default=0, help="accumulate_tail (0 = rule, -1 = none)")
 p.add_argument("--tail-chunk", type=int, default=0)
+p.add_argument("--quantum", type=int, default=0, help="accumulate_quantum (0 = the rule)")
 a = p.parse_args()
 base = dict(width=1920, height=1080, samples_per_pixel=a.spp, max_depth=10, device=0,
             accumulate_chunk=a.chunk, kernel_variant=a.variant, code_object_path=a.code_object,
-            accumulate_tail=a.tail, accumulate_tail_chunk=a.tail_chunk)
+            accumulate_tail=a.tail, accumulate_tail_chunk=a.tail_chunk,
+            accumulate_quantum=a.quantum)
 # steady state: the second frame of each renderer (the first after Begin runs ~5% slower)
 with vc.Renderer(vc.RenderDesc(**base), "final") as r:
     r.draw_next_frame()

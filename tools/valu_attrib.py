@@ -1,23 +1,25 @@
-"""VALU attribution of the flat tracer kernel by phase.
+"""VALU attribution of the flat tracer kernel by phase (static instruction counts beside the
+stats build's measured phase shares).
 
 Static part: every instruction of a kernel in a line-table build of the code object
 (-gline-tables-only, whose instruction stream this tool checks is identical to the product code
 object's) is symbolized with its inline chain (llvm-symbolizer --inlining) and assigned to a
 phase of trace_impl (camera fast trace: big list / listed spheres / roots; main scan: ray set-up,
-big list, node level, passes by kind; shading: sine / rest / sky; retire; fetch; loop control).
+big list, node level, passes by kind; shading: sines / normal and scatter / sky / next camera
+ray; retire; fetch; loop control). Rare fallback code (the canonical sine, hipcc's full sqrt and
+division sequences, the linear scan of unguarded waves) is listed under its own phase.
 
-Dynamic part: rocprofv3 stochastic PC samples (--pc-sampling-method stochastic, unit cycles) of
-the product kernel, taken at uniform cycle intervals per wave; a sample that issued a VALU
-instruction counts one VALU issue slot at its PC. Their shares, scaled to the kernel's
-SQ_INSTS_VALU (profiles/traffic.json), give VALU instructions per phase.
+With --phases (the JSON of a stats-build frame, VCRT_DEBUG_STATS=1 tools/render_once.py: wave
+clock per phase, pass and loop trip counts) and --sq-valu (SQ_INSTS_VALU per wave-segment of the
+product at the same workload, profiles/traffic.json), it prints the measured time shares beside
+the static counts. This is an estimate: PC sampling is not available on the GPU pool, and the
+product kernel is not instrumented; the stats build's clocks include memory waits.
 
-  python tools/valu_attrib.py --hsaco LINE_TABLE.hsaco --product lib/vcrt_tracer.hsaco \
-      [--kernel vcrt_trace_cull_flat] [--pcs gpurun_out/pcs/.../pcs_pc_sampling_stochastic.csv]
+  python tools/valu_attrib.py --hsaco LINE_TABLE.hsaco [--kernel vcrt_trace_cull_flat]
+      [--phases gpurun_out/phases.json] [--sq-valu 753.2]
 """
 import argparse
-import bisect
 import collections
-import csv
 import json
 import os
 import re
@@ -97,6 +99,9 @@ def marker_lines():
     m["scan"] = find("// ---- one segment: scan the whole sphere list", m["cam_shade"])
     m["shade"] = find("// ---- shade (textures.glsl)", m["scan"])
     m["end"] = find("VCRT_WAVE_END_TIMES", m["shade"])
+    # the real branches of the rare fallbacks (asm volatile(""): not if-converted)
+    m["rare"] = {find("r = __builtin_sqrtf(x);"), find("sq = __builtin_sqrtf(disc);"),
+                 find("normal = divs(pcv, cr.w);")}
     return m
 
 
@@ -104,14 +109,18 @@ def phase(chain, mk):
     """The phase of one instruction from its inline chain (innermost first)."""
     fns = [f for f, _, _ in chain]
     text = " | ".join(fns)
+    if any(k in text for k in ("sin_canonical", "ksin", "kcos", "reduce_large")):
+        return "rare: canonical sine (fallback of the fast sine)"
+    if any(fl == "tracer.hip" and ln in mk["rare"] for _, fl, ln in chain):
+        return "rare: full sqrt / division (fallbacks)"
     impl = [(f, fl, ln) for f, fl, ln in chain if f.startswith("trace_impl")]
     line = impl[0][2] if impl else 0
     # shade_and_advance (its body lies between its definition and the loop; the other lambda,
     # pixel_corner, counts where it is called)
     lam = [ln for f, _, ln in chain if f == "operator()" and mk["lam"] <= ln < mk["loop"]]
     if lam:  # shade_and_advance (the lambda)
-        if any(k in text for k in ("sin3", "sin_fast_try", "sin_canonical", "ksin", "kcos")):
-            return "shading: the three sines"
+        if any(k in text for k in ("sin3", "sin_fast_try")):
+            return "shading: the three sines (fast path)"
         ln = lam[0]
         if mk["lam_sky"] <= ln < mk["lam_end"]:
             return "shading: sky"
@@ -137,7 +146,7 @@ def phase(chain, mk):
             return "scan: node level (chunk's 8 node boxes)"
         return "scan: set-up, lists, pushes, key"
     if "scan_spheres" in text:
-        return "scan: linear fallback"
+        return "rare: linear scan (waves outside the guarded range)"
     if not impl:
         return "other"
     if "exact_group_uniform_cam" in text:
@@ -167,37 +176,21 @@ def is_valu(mn):
     return mn.startswith("v_")
 
 
-def load_pcs(path, base):
-    """PC samples of the kernel -> Counter(offset within the code object -> (all, valu issued))."""
-    allc, valu = collections.Counter(), collections.Counter()
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            off = None
-            for k in ("Instruction_Comment", "Code_Object_Offset", "code_object_offset"):
-                if k in row and row[k]:
-                    try:
-                        off = int(row[k], 0)
-                    except ValueError:
-                        pass
-            if off is None:
-                continue
-            allc[off] += 1
-            issued = row.get("Wave_Issued_Instruction", row.get("wave_issued", "1"))
-            itype = row.get("Instruction_Type", row.get("inst_type", ""))
-            if str(issued) in ("1", "True", "true") and "VALU" in itype.upper():
-                valu[off] += 1
-    return allc, valu
-
-
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--hsaco", required=True, help="-gline-tables-only build of tracer.hip")
+    p.add_argument("--hsaco", default=None, help="-gline-tables-only build of tracer.hip "
+                   "(default: built now from the current source into ab_objs/lt.hsaco)")
     p.add_argument("--product", default=os.path.join(ROOT, "vulkancomputeraytracing_amd", "lib",
                                                      "vcrt_tracer.hsaco"))
     p.add_argument("--kernel", default="vcrt_trace_cull_flat")
-    p.add_argument("--pcs", default=None)
+    p.add_argument("--phases", default=None)
+    p.add_argument("--sq-valu", type=float, default=None)
     p.add_argument("--json", default=None)
     a = p.parse_args()
+    if a.hsaco is None:  # the line tables must come from the source the markers are read from
+        a.hsaco = subprocess.run(["bash", os.path.join(ROOT, "tools", "mkab.sh"), "lt"],
+                                 env=dict(os.environ, EXTRA="-gline-tables-only"),
+                                 capture_output=True, text=True, check=True).stdout.strip()
     insts = disasm(a.hsaco, a.kernel)
     prod = disasm(a.product, a.kernel)
     same = normalized(insts) == normalized(prod)
@@ -219,33 +212,36 @@ def main():
     print("static VALU instructions by phase:")
     for ph, n in static.most_common():
         print(f"  {n:5d}  {ph}")
-    if a.pcs:
-        allc, valu = load_pcs(a.pcs, insts[0][0])
-        addrs = [ad for ad, _, _ in insts]
-        lo, hi = addrs[0], addrs[-1]
-        # offsets may be absolute code-object offsets (within the kernel's range) or
-        # kernel-relative; take whichever puts the samples inside the kernel
-        rel = sum(v for k, v in allc.items() if lo <= k <= hi) < sum(
-            v for k, v in allc.items() if k <= hi - lo)
-        dyn_all, dyn_valu = collections.Counter(), collections.Counter()
-        miss = 0
-        for src, dst in ((allc, dyn_all), (valu, dyn_valu)):
-            for off, n in src.items():
-                ad = off + lo if rel else off
-                i = bisect.bisect_right(addrs, ad) - 1
-                if i < 0 or ad > hi + 8:
-                    miss += n
-                    continue
-                dst[ph_of[addrs[i]]] += n
-        tv, ta = sum(dyn_valu.values()), sum(dyn_all.values())
-        print(f"PC samples: {ta} in the kernel ({miss} outside), {tv} issuing VALU")
-        for ph, n in dyn_valu.most_common():
-            print(f"  {100.0 * n / max(tv, 1):5.1f}% of VALU issues  "
-                  f"{100.0 * dyn_all[ph] / max(ta, 1):5.1f}% of samples  {ph}")
-        res["pc_samples"] = ta
-        res["pc_valu_samples"] = tv
-        res["valu_share"] = {ph: n / max(tv, 1) for ph, n in dyn_valu.most_common()}
-        res["sample_share"] = {ph: n / max(ta, 1) for ph, n in dyn_all.most_common()}
+    if a.phases:
+        st = json.load(open(a.phases))
+        d = st["debug"]
+        wi, tot = d[0], d[14]
+        shares = [("camera fast trace (shading excluded)", d[23] - d[3]),
+                  ("camera-phase shading", d[3]), ("main scan: big list", d[15]),
+                  ("main scan: node level", d[9]), ("main scan: node pushes", d[16]),
+                  ("main scan: node passes", d[10]), ("main scan: group passes", d[11]),
+                  ("main scan: candidate passes", d[12]),
+                  ("main scan: rest (ray set-up, lists, key, drain)",
+                   d[8] - d[15] - d[9] - d[16] - d[10] - d[11] - d[12]),
+                  ("main-scan sky shading", d[17]), ("fetch", d[18])]
+        rest = tot - sum(v for _, v in shares)
+        shares.append(("loop, retire, hand-over", rest))
+        print(f"stats build: {wi} wave-iterations, {st['segments']} segments, "
+              f"{st['segments'] / 64 / wi:.2f} wave-segments per wave-iteration")
+        print("measured wave-time shares (stats build, s_memtime per phase):")
+        res["time_share"] = {}
+        for name, v in shares:
+            print(f"  {100.0 * v / tot:5.1f}%  {name}")
+            res["time_share"][name] = v / tot
+        res["wave_iterations"] = wi
+        res["segments"] = st["segments"]
+        if a.sq_valu:
+            per_iter = a.sq_valu * st["segments"] / 64 / wi
+            print(f"product VALU per wave-iteration (SQ_INSTS_VALU {a.sq_valu} per wave-segment): "
+                  f"{per_iter:.0f}; by time share:")
+            for name, v in shares:
+                print(f"  {per_iter * v / tot:6.0f}  {name}")
+            res["valu_per_iteration"] = per_iter
     if a.json:
         json.dump(res, open(a.json, "w"), indent=1)
 

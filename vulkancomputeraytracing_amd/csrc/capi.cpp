@@ -177,11 +177,15 @@ uint32_t tiles_for_rank(int32_t width, int32_t height, int32_t world, int32_t ra
 // The accumulation quantum G (vcrt.h accumulate_quantum): the image depends on G alone. A
 // pixel's samples are summed in fp32 within each run of G consecutive samples, and the runs'
 // sums are quantized and added exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks of
-// them per pixel: 16, doubled while the frame's samples would need more. G does not depend on
+// them per pixel: 4, doubled while the frame's samples would need more. G does not depend on
 // the number of GPUs, so a sharded frame equals the one-GPU frame bit for bit with default descs
 // (round 4; before, the chunk was the quantum and followed the rank's share: K = 64 on one GPU,
-// 16 at N = 8, so the default images differed). Work items (chunks, the tail) hold whole quanta.
-constexpr int32_t kDefaultQuantum = 16;
+// 16 at N = 8, so the default images differed). Work items (chunks, the tail) hold whole quanta,
+// so G bounds the tail's item size from below, which sets the drain at N = 8: with G = 4 the
+// default partitions are round 3's (K = 64 + 64 x 8 on one GPU, K = 16 + 128 x 4 at N = 8);
+// measured at C4, the 8-way max rank 13.42 / 13.48 / 14.39 ms with G = 4 / 8 / 16, and the one-GPU
+// frame within 0.5% for the three (profiles/r04_ab_log.md).
+constexpr int32_t kDefaultQuantum = 4;
 
 int32_t work_quantum(const vcrt_render_desc& d) {
     if (d.accumulate_quantum > 0) return d.accumulate_quantum;
@@ -232,12 +236,13 @@ int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk)
         t = 1 << static_cast<int>(std::lround(std::log2(raw)));  // nearest power of two
         if (4 * static_cast<int64_t>(t) > spp) return 0;
     }
-    // whole quanta: the head ends on a quantum boundary (the tail grows to it), tail items are
-    // one quantum (the rule) or whole quanta, the last one ending at spp
+    // whole quanta: the head ends on a quantum boundary (the tail grows to it), tail items of
+    // max(4, K / 8) samples (the rule) or as given, rounded up to whole quanta, the last one
+    // ending at spp
     const int32_t head_end = (spp - t) / q * q;
     if (head_end <= 0) return 0;
     t = spp - head_end;
-    kt = kt <= 0 ? q : round_up(kt, q);
+    kt = round_up(kt <= 0 ? std::max(4, chunk / 8) : kt, q);
     *tail_chunk = std::min(kt, t);
     return t;
 }

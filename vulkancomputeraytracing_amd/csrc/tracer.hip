@@ -276,6 +276,38 @@ __device__ __forceinline__ float sqrt_unscaled(float x) {
     return __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
 }
 
+// Correctly rounded x / a by div_a's unscaled sequence where it gives hipcc's bits: a in
+// [2^-20, 2^20] and |x| in [2^-103, 2^64), so that x, a and x / a are normal, exp(x) > 23 and
+// exp(x) - exp(a) < 96 (the conditions under which v_div_scale and v_div_fmas leave the operands
+// unscaled, see candidate_t_fast), or x = +-0, whose quotient both sequences give as a zero of
+// the right sign (q0 = x y and the residuals fma(-a, q, x) are zeros that keep it); else hipcc's
+// full division in a real branch. Round 4: normalize(u) in the Lambertian / metal scatter (u's
+// components are fract values in [0, 1), often exactly 0, which round 2's range check sent to
+// the full path) and the sky's y / |d|.
+__device__ __forceinline__ bool div_fast_ok(float x, float a) {
+    const float ax = fabsf(x);
+    return a >= 0x1p-20f && a <= 0x1p20f && ((ax >= 0x1p-103f && ax < 0x1p64f) || ax == 0.0f);
+}
+
+__device__ __forceinline__ float div1_fast(float x, float a) {
+    float q = div_a(x, a, recip_a(a));
+    if (!div_fast_ok(x, a)) {
+        asm volatile("");
+        q = x / a;
+    }
+    return q;
+}
+
+__device__ __forceinline__ f3 div3_fast(f3 v, float a) {
+    const float ya = recip_a(a);
+    f3 q = mk(div_a(v.x, a, ya), div_a(v.y, a, ya), div_a(v.z, a, ya));
+    if (!(div_fast_ok(v.x, a) && div_fast_ok(v.y, a) && div_fast_ok(v.z, a))) {
+        asm volatile("");
+        q = divs(v, a);
+    }
+    return q;
+}
+
 // Correctly rounded sqrt for any x: the unscaled sequence, and hipcc's full one in a real branch
 // for lanes outside [2^-96, inf] (tiny, zero, negative or NaN x).
 __device__ __forceinline__ float sqrt_fast(float x) {
@@ -1513,7 +1545,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 const float r2 = rand_of_sin(s2);
                 const float r3 = rand_of_sin(s3);
                 const f3 ru = mk(r1, r2, r3);  // random_in_unit_sphere(dir): normalize
-                const f3 u = divs(ru, sqrt_fast(dot(ru, ru)));
+                const f3 u = div3_fast(ru, sqrt_fast(dot(ru, ru)));
                 if (type == 1) {
                     d = add(normal, u);
                     atten = scale(param, mul(atten, albedo));
@@ -1552,7 +1584,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             if (pass >= P.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
         } else {
             const float len = sqrt_fast(dot(d, d));  // length(d)
-            contrib = mul(atten, sky_factor(d.y / len));
+            contrib = mul(atten, sky_factor(div1_fast(d.y, len)));
             ended = true;
         }
 
