@@ -13,6 +13,9 @@
 #   profile     the round's profile set for tools/collect_profile.py $TAG: bench lines (c4 c3 c2
 #               c5), rocprofv3 --kernel-trace --stats of each bench command, and PMC passes (one
 #               counter block per run: FETCH_SIZE, WRITE_SIZE, two SQ sets) of one frame of each
+#   pmcab       instruction counters of one frame ($PMC_CFG, default c4) for the prev tree ($PREV),
+#               the current tree and the code objects in $OBJS: two PMC passes each, summarised by
+#               tools/pmc_ab_summary.py (VALU per wave-segment, issue, lane utilisation)
 #   phases      stats build (VCRT_DEBUG_STATS=1): s_memtime per phase of the flat scan ($RO args)
 #   wavetimes   diagnostics build $WT_OBJ (VCRT_DEBUG_STATS=2): wave lifetimes ($WT_ARGS)
 set -o pipefail
@@ -111,6 +114,33 @@ mode_profile() {
       || { echo "pmc $c failed"; return 1; }
   done
   echo profile_done
+}
+
+mode_pmcab() {
+  local P=$OUT/pmcab RO=$(cfg_args ${PMC_CFG:-c4})
+  rm -rf $P && mkdir -p $P
+  local S1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+  local S2="SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM"
+  pmc_one() {  # tag, env prefix / extra render_once args...
+    local tag=$1 env=$2; shift 2
+    for pass in 1 2; do
+      local C=$S1; [ $pass = 2 ] && C=$S2
+      (cd /tmp && export $env && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv \
+        -d $P/${tag}_$pass -o run -- python3 $ROOT/tools/render_once.py $RO "$@" \
+        > $P/${tag}_$pass.log 2>&1) || { tail -5 $P/${tag}_$pass.log; return 1; }
+    done
+  }
+  if [ -n "$PREV" ]; then pmc_one prev VCRT_PKG_ROOT=$ROOT/$PREV || return 1; fi
+  pmc_one new VCRT_OBJ=none || return 1
+  local i=0
+  for o in $OBJS; do  # a code object, or args:A,B (render_once arguments with the current one)
+    i=$((i+1))
+    case $o in
+      args:*) pmc_one obj$i VCRT_OBJ=args $(echo ${o#args:} | tr , ' ') || return 1;;
+      *) pmc_one obj$i VCRT_OBJ=$o --code-object $ROOT/$o || return 1;;
+    esac
+  done
+  python tools/pmc_ab_summary.py $P
 }
 
 mode_phases() {

@@ -27,8 +27,9 @@ def counters(d):
 
 def stats(log):
     for line in open(log):
-        if line.startswith("["):
-            return json.loads(line)[-1]
+        if line.startswith("[") or line.startswith("{"):
+            st = json.loads(line)
+            return st[-1] if isinstance(st, list) else st
     return None
 
 

@@ -5,7 +5,9 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# VCRT_PKG_ROOT: the package (and its libvcrt.so) of another tree (tools/mkab_tree.sh), for A/B
+sys.path.insert(0, os.environ.get("VCRT_PKG_ROOT",
+                                  os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import vulkancomputeraytracing_amd as vc  # noqa: E402
 
@@ -26,6 +28,7 @@ def main():
     p.add_argument("--world", type=int, default=1)
     p.add_argument("--tail", type=int, default=0, help="accumulate_tail (0 = rule, -1 = none)")
     p.add_argument("--tail-chunk", type=int, default=0)
+    p.add_argument("--quantum", type=int, default=0, help="accumulate_quantum (0 = rule)")
     a = p.parse_args()
     desc = vc.RenderDesc(width=a.width, height=a.height, samples_per_pixel=a.spp,
                          max_depth=a.depth, kernel_variant=a.variant,
@@ -33,6 +36,8 @@ def main():
                          code_object_path=a.code_object, accumulate_chunk=a.chunk,
                          rank=a.rank, world_size=a.world, accumulate_tail=a.tail,
                          accumulate_tail_chunk=a.tail_chunk)
+    if a.quantum:
+        desc.accumulate_quantum = a.quantum
     with vc.Renderer(desc, a.scene) as r:
         out = []
         for _ in range(a.frames):

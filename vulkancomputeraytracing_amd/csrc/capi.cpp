@@ -58,7 +58,7 @@ struct RendererState {
                   k_trace_cull_lane_lds_wide_stats = nullptr, k_trace_cull_flat = nullptr,
                   k_trace_cull_flat_stats = nullptr, k_trace_cull_flat_global = nullptr,
                   k_trace_cull_flat_global_stats = nullptr, k_trace_cull_flat_boxes = nullptr,
-                  k_trace_cull_flat_boxes_stats = nullptr;
+                  k_trace_cull_flat_boxes_stats = nullptr, k_setup_jitter = nullptr;
     // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global, 3 = boxes in LDS (flat scan)
     int cull_lane_tables = 0;
     bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
@@ -103,7 +103,8 @@ struct RendererState {
     float* d_srgb_thresholds = nullptr;
     uchar4* d_srgb = nullptr;
     // per-frame inputs / outputs
-    float2* d_jitter = nullptr;
+    float2* d_jitter_in = nullptr;  // the host's jitter (jx, jy) of the frame's sample indices
+    float4* d_jitter = nullptr;     // TraceParams.jitter (vcrt_setup_jitter)
     float4* d_fb_own = nullptr;
     float4* d_fb = nullptr;  // current render target (own or caller-provided)
     size_t fb_bytes = 0;
@@ -355,6 +356,7 @@ VkResult bind_kernels() {
     VCRT_TRY(hipModuleGetFunction(&g.k_fill, m, "vcrt_fill"));
     VCRT_TRY(hipModuleGetFunction(&g.k_resolve, m, "vcrt_resolve"));
     VCRT_TRY(hipModuleGetFunction(&g.k_encode, m, "vcrt_encode_srgb8"));
+    VCRT_TRY(hipModuleGetFunction(&g.k_setup_jitter, m, "vcrt_setup_jitter"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_lds_stats, m, "vcrt_trace_lds_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull, m, "vcrt_trace_cull"));
@@ -442,6 +444,27 @@ template <typename Params>
 VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Params& params) {
     void* args[] = {&params};
     VCRT_TRY(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, lds, g.stream, args, nullptr));
+    return VK_SUCCESS;
+}
+
+// TraceParams.jitter (vcrt_kernel_abi.h SetupJitterParams): the jitter term of the frame's
+// sample indices base .. base + spp - 1 (shader.comp:48), on the device with the tracer's own
+// operations.
+VkResult setup_jitter(uint64_t base) {
+    const int spp = g.desc.samples_per_pixel;
+    make_jitter(base, spp, g.jitter_host);
+    VCRT_TRY(hipMemcpyAsync(g.d_jitter_in, g.jitter_host.data(), sizeof(float2) * spp,
+                            hipMemcpyHostToDevice, g.stream));
+    vcrt::SetupJitterParams sp{};
+    sp.jitter_in = g.d_jitter_in;
+    sp.jitter = g.d_jitter;
+    sp.nsamples = static_cast<uint32_t>(spp);
+    const std::array<float, 12> cam = camera_array();
+    for (int i = 0; i < 12; i++) sp.cam[i] = cam[i];
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((spp + 255) / 256, 1024));
+    VkResult r = launch(g.k_setup_jitter, grid, 256, 0, sp);
+    if (r != VK_SUCCESS) return r;
+    VCRT_TRY(hipStreamSynchronize(g.stream));  // jitter_host is reused by the next frame
     return VK_SUCCESS;
 }
 
@@ -739,11 +762,9 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
                               [](double x) { return std::tan(x); });
     // Jitter (shader.comp:48) depends only on the sample index: one table per frame config.
     const int spp = g.desc.samples_per_pixel;
-    make_jitter(0, spp, g.jitter_host);
-    if ((r = to_vk(hipMalloc(&g.d_jitter, sizeof(float2) * spp))) != VK_SUCCESS) return fail(r);
-    if ((r = to_vk(hipMemcpy(g.d_jitter, g.jitter_host.data(), sizeof(float2) * spp,
-                             hipMemcpyHostToDevice))) != VK_SUCCESS)
-        return fail(r);
+    if ((r = to_vk(hipMalloc(&g.d_jitter_in, sizeof(float2) * spp))) != VK_SUCCESS) return fail(r);
+    if ((r = to_vk(hipMalloc(&g.d_jitter, sizeof(float4) * spp))) != VK_SUCCESS) return fail(r);
+    if ((r = setup_jitter(0)) != VK_SUCCESS) return fail(r);
     {
         float th[255];
         srgb_thresholds(th);
@@ -1016,10 +1037,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
     if (g.desc.progressive && g.accumulated > 0) {
         // progressive frames continue the sample sequence: indices accumulated.. (+spp)
-        make_jitter(g.accumulated, g.desc.samples_per_pixel, g.jitter_host);
-        VCRT_TRY(hipMemcpyAsync(g.d_jitter, g.jitter_host.data(),
-                                sizeof(float2) * g.jitter_host.size(), hipMemcpyHostToDevice,
-                                g.stream));
+        const VkResult rj = setup_jitter(g.accumulated);
+        if (rj != VK_SUCCESS) return rj;
     }
     if (pixels != 0 && g.desc.max_depth > 0) {
         vcrt::TraceParams p{};
@@ -1079,7 +1098,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.stage_spp = 0u;
         if (kc.f == g.k_trace_smem && g.nspheres > 0 && g.stage_tables) {
             const uint32_t bytes = 48u * static_cast<uint32_t>(g.nspheres) +
-                                   8u * static_cast<uint32_t>(g.desc.samples_per_pixel);
+                                   16u * static_cast<uint32_t>(g.desc.samples_per_pixel);
             if (bytes <= kStageMaxBytes) {
                 p.stage_spheres = static_cast<uint32_t>(g.nspheres);
                 p.stage_spp = static_cast<uint32_t>(g.desc.samples_per_pixel);
@@ -1210,6 +1229,7 @@ vcrt_result vcrt_end(void) {
     if (g.stream) (void)hipStreamSynchronize(g.stream);
     free_scene();
     if (g.d_jitter) (void)hipFree(g.d_jitter);
+    if (g.d_jitter_in) (void)hipFree(g.d_jitter_in);
     if (g.d_fb_own) (void)hipFree(g.d_fb_own);
     if (g.d_counters) (void)hipFree(g.d_counters);
     if (g.d_debug) (void)hipFree(g.d_debug);
@@ -1346,10 +1366,7 @@ vcrt_result vcrt_reset_accumulation(void) {
     VCRT_TRY(hipStreamSynchronize(g.stream));
     if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
     g.accumulated = 0;
-    make_jitter(0, g.desc.samples_per_pixel, g.jitter_host);
-    VCRT_TRY(hipMemcpy(g.d_jitter, g.jitter_host.data(), sizeof(float2) * g.jitter_host.size(),
-                       hipMemcpyHostToDevice));
-    return VCRT_SUCCESS;
+    return setup_jitter(0);
 }
 
 vcrt_result vcrt_selftest_sin(uint32_t first, uint32_t count, uint64_t* mismatches,

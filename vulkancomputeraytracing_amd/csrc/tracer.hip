@@ -276,38 +276,6 @@ __device__ __forceinline__ float sqrt_unscaled(float x) {
     return __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
 }
 
-// Correctly rounded x / a by div_a's unscaled sequence where it gives hipcc's bits: a in
-// [2^-20, 2^20] and |x| in [2^-103, 2^64), so that x, a and x / a are normal, exp(x) > 23 and
-// exp(x) - exp(a) < 96 (the conditions under which v_div_scale and v_div_fmas leave the operands
-// unscaled, see candidate_t_fast), or x = +-0, whose quotient both sequences give as a zero of
-// the right sign (q0 = x y and the residuals fma(-a, q, x) are zeros that keep it); else hipcc's
-// full division in a real branch. Round 4: normalize(u) in the Lambertian / metal scatter (u's
-// components are fract values in [0, 1), often exactly 0, which round 2's range check sent to
-// the full path) and the sky's y / |d|.
-__device__ __forceinline__ bool div_fast_ok(float x, float a) {
-    const float ax = fabsf(x);
-    return a >= 0x1p-20f && a <= 0x1p20f && ((ax >= 0x1p-103f && ax < 0x1p64f) || ax == 0.0f);
-}
-
-__device__ __forceinline__ float div1_fast(float x, float a) {
-    float q = div_a(x, a, recip_a(a));
-    if (!div_fast_ok(x, a)) {
-        asm volatile("");
-        q = x / a;
-    }
-    return q;
-}
-
-__device__ __forceinline__ f3 div3_fast(f3 v, float a) {
-    const float ya = recip_a(a);
-    f3 q = mk(div_a(v.x, a, ya), div_a(v.y, a, ya), div_a(v.z, a, ya));
-    if (!(div_fast_ok(v.x, a) && div_fast_ok(v.y, a) && div_fast_ok(v.z, a))) {
-        asm volatile("");
-        q = divs(v, a);
-    }
-    return q;
-}
-
 // Correctly rounded sqrt for any x: the unscaled sequence, and hipcc's full one in a real branch
 // for lanes outside [2^-96, inf] (tiny, zero, negative or NaN x).
 __device__ __forceinline__ float sqrt_fast(float x) {
@@ -1315,13 +1283,23 @@ __device__ __forceinline__ Pixel pixel_of(uint32_t q, uint32_t W, uint32_t H, ui
     return px;
 }
 
-// The jitter of sample i (shader.comp:48) and a hit sphere's shading rows, from the LDS copy the
-// SMEM scan stages for small scenes (TraceParams.stage_*), else from global memory.
+// The viewport point's two terms, each one fixed sequence of fp32 operations: shader.comp:43's
+// pixel corner pixel00 + x delta_u + y delta_v, and :48-49's jitter in world units
+// jx delta_u + jy delta_v (TraceParams.jitter); the sample's point is their sum.
+__device__ __forceinline__ f3 viewport_corner(f3 p00, f3 du, f3 dv, uint32_t x, uint32_t y) {
+    return add(add(p00, scale((float)x, du)), scale((float)y, dv));
+}
+
+__device__ __forceinline__ f3 viewport_jitter(f3 du, f3 dv, float2 jt) {
+    return add(scale(jt.x, du), scale(jt.y, dv));
+}
+
+// The jitter term of sample i and a hit sphere's shading rows, from the LDS copy the SMEM scan
+// stages for small scenes (TraceParams.stage_*), else from global memory.
 template <bool kStageable>
-__device__ __forceinline__ float2 jitter_at(const TraceParams& p, const float4* lds, int i) {
+__device__ __forceinline__ float4 jitter_at(const TraceParams& p, const float4* lds, int i) {
     if constexpr (kStageable) {
-        if (p.stage_spp != 0u)
-            return reinterpret_cast<const float2*>(lds + 3u * p.stage_spheres)[i];
+        if (p.stage_spp != 0u) return lds[3u * p.stage_spheres + (uint32_t)i];
     }
     return p.jitter[i];
 }
@@ -1375,8 +1353,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 lds_dyn[ns + i] = P.shade[i];
                 lds_dyn[2u * ns + i] = P.material[i];
             }
-            float2* jd = reinterpret_cast<float2*>(lds_dyn + 3u * ns);
-            for (uint32_t i = threadIdx.x; i < P.stage_spp; i += blockDim.x) jd[i] = P.jitter[i];
+            for (uint32_t i = threadIdx.x; i < P.stage_spp; i += blockDim.x)
+                lds_dyn[3u * ns + i] = P.jitter[i];
             __syncthreads();
         }
     }
@@ -1471,10 +1449,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     uint32_t q = 0;
     uint32_t pxy = 0;  // the item's pixel: y << 16 | x
     f3 o = mk(0.f, 0.f, 0.f), d = o, atten = o, acc = o;
-    // shader.comp:43  pixel00 + x*delta_u + y*delta_v, recomputed from pxy at each sample start
-    // (three VGPRs fewer across the loop than keeping it)
-    auto pixel_corner = [&]() {
-        return add(add(p00, scale((float)(pxy & 0xffffu), du)), scale((float)(pxy >> 16), dv));
+    // shader.comp:43-52: the camera ray of sample s of the lane's pixel, (corner + jitter) - center,
+    // the jitter term from its table (the same operations, done once per sample index instead of
+    // at every sample start; a table of the pixel corners as well measured no faster: its loads
+    // cost what its VALU savings gained). The corner is recomputed from pxy (three VGPRs fewer
+    // across the loop than keeping it).
+    auto camera_dir = [&](int s) {
+        const f3 c = viewport_corner(p00, du, dv, pxy & 0xffffu, pxy >> 16);
+        const float4 j = jitter_at<kStageable>(P, lds_dyn, s);
+        return sub(add(c, mk(j.x, j.y, j.z)), cam);
     };
     uint32_t segs = 0;  // this lane's segments (< 2^32: ~2.4e5 per lane at the C5 workload)
     uint64_t st_iters = 0, st_active = 0, st_hitgroups = 0, st_fetch = 0;
@@ -1545,7 +1528,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 const float r2 = rand_of_sin(s2);
                 const float r3 = rand_of_sin(s3);
                 const f3 ru = mk(r1, r2, r3);  // random_in_unit_sphere(dir): normalize
-                const f3 u = div3_fast(ru, sqrt_fast(dot(ru, ru)));
+                const f3 u = divs(ru, sqrt_fast(dot(ru, ru)));
                 if (type == 1) {
                     d = add(normal, u);
                     atten = scale(param, mul(atten, albedo));
@@ -1584,7 +1567,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             if (pass >= P.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
         } else {
             const float len = sqrt_fast(dot(d, d));  // length(d)
-            contrib = mul(atten, sky_factor(div1_fast(d.y, len)));
+            contrib = mul(atten, sky_factor(d.y / len));
             ended = true;
         }
 
@@ -1601,10 +1584,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // a quantum of G samples ends inside the item: its sum is retired the same way,
                 // and the item goes on with its next sample
                 if (((uint32_t)sample & P.quantum_mask) == 0u) fin = true;
-                const float2 jt = jitter_at<kStageable>(P, lds_dyn, sample);
-                const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
+                d = camera_dir(sample);
                 o = cam;
-                d = sub(ps, cam);
                 atten = mk(1.f, 1.f, 1.f);
                 pass = 0;
                 fresh_cam = true;
@@ -1647,10 +1628,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 const double v1 = (double)__builtin_rintf(ay * kAccumScale);
                 const double v2 = (double)__builtin_rintf(az * kAccumScale);
                 const uint32_t qi = q & kQMask, ent = q >> kRingQBits;
-                // the pixel's ring entry while it still holds this pixel (LDS atomics), else
+                // the pixel's ring entry while it still holds this pixel (LDS atomics; a claim
+                // that takes the entry for another pixel clears the lane's entry field), else
                 // global memory (two branches: a pointer that may be either would make flat
                 // atomics, whose completion every later LDS wait would wait for)
-                if (ent != 0u && ring[ent - 1u].q == qi) {
+                if (ent != 0u) {
                     double* s = ring[ent - 1u].s;
                     atomicAdd(s + 0, v0);
                     atomicAdd(s + 1, v1);
@@ -1725,6 +1707,17 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                                        blk_lt, (blk_ty << 16) | blk_tx, (uint32_t)P.width,
                                        (uint32_t)P.height);
                         __builtin_amdgcn_wave_barrier();
+                        // a lane whose item's entry is among those just claimed (its own, or
+                        // the one of an item handed to it earlier in this fetch) loses it: the
+                        // item's later quanta go to global memory
+                        const uint32_t rn = P.ring_n, pos = ring_pos;
+                        auto keep = [rn, pos, np](uint32_t ent) {
+                            uint32_t rel = ent + rn - 1u - pos;
+                            if (rel >= rn) rel -= rn;
+                            return (ent != 0u && rel < np) ? 0u : ent;
+                        };
+                        q = (q & kQMask) | (keep(q >> kRingQBits) << kRingQBits);
+                        g_ent = keep(g_ent);
                         blk_ps0 = ps0;
                         blk_ring = ring_pos + 1u;
                         ring_pos += np;
@@ -1770,10 +1763,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             sample = (tail ? P.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
             sample_end = min(sample + k, tail ? P.spp : P.tail_start);
             // first camera ray of the chunk, shader.comp:48-52
-            const float2 jt = jitter_at<kStageable>(P, lds_dyn, sample);
-            const f3 ps = add(pixel_corner(), add(scale(jt.x, du), scale(jt.y, dv)));
+            d = camera_dir(sample);
             o = cam;
-            d = sub(ps, cam);
             atten = mk(1.f, 1.f, 1.f);
             pass = 0;
             fresh = true;
@@ -1841,7 +1832,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     }
                     // ...then the candidates' roots, one per lane and loop trip (the wave runs
                     // as many trips as its busiest lane has candidates, mostly one), with the
-                    // sphere's hb and disc recomputed by the same operations
+                    // sphere's hb and disc recomputed by the same operations (measured: both
+                    // members' roots packed in the first loop issue more VALU, +1.8%)
                     while (cbits) {
                         const uint32_t b = (uint32_t)__builtin_ctz(cbits);
                         cbits &= cbits - 1u;
@@ -2180,6 +2172,17 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) 
         const double4 s = *reinterpret_cast<const double4*>(p.accum + 4u * q);
         p.out[px.out_index] = make_float4(resolve_channel(s.x, st), resolve_channel(s.y, st),
                                           resolve_channel(s.z, st), 1.0f);
+    }
+}
+
+// TraceParams.jitter (SetupJitterParams): the jitter term of every sample index.
+extern "C" __global__ __launch_bounds__(256) void vcrt_setup_jitter(SetupJitterParams p) {
+    const f3 du = mk(p.cam[3], p.cam[4], p.cam[5]);
+    const f3 dv = mk(p.cam[6], p.cam[7], p.cam[8]);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.nsamples;
+         i += gridDim.x * blockDim.x) {
+        const f3 v = viewport_jitter(du, dv, p.jitter_in[i]);
+        p.jitter[i] = make_float4(v.x, v.y, v.z, 0.0f);
     }
 }
 

@@ -25,7 +25,11 @@ struct TraceParams {
     const float4* shade;          // [n] (colour.rgb, texture.y = param)
     const float4* material;       // [n] (texture.x = material id, 1 / texture.y, Schlick r0^2
                                   //   of texture.y, 0): the glass quotients precomputed (fp32)
-    const float2* jitter;  // [spp] (-0.5+rand(i,i), -0.5+rand(i+1,i+1)), shader.comp:48
+    // shader.comp:43-49's viewport point pixel00 + x delta_u + y delta_v + jx delta_u + jy delta_v
+    // is the sum of two fp32 terms: the pixel's corner (computed at each sample start) and the
+    // sample's jitter term, a table (vcrt_setup_jitter, the kernel's own operations)
+    const float4* jitter;  // [spp] jx delta_u + jy delta_v, (jx, jy) = (-0.5+rand(i,i),
+                           //   -0.5+rand(i+1,i+1)) of sample index i (shader.comp:48)
     float4* out;           // rank-local framebuffer, rgba32f (layout above)
     double* accum;         // [local_tiles * 64][4] exact sums of the quantized chunk sums (r, g,
                            //   b, unused), vcrt_math.h "Accumulation"; unused with kFlagDirect
@@ -91,7 +95,7 @@ struct TraceParams {
     uint32_t ring_off, ring_n;
     // The linear SMEM scan's staging (small scenes, C2): when stage_spp != 0 the kernel copies
     // the shading tables of the stage_spheres spheres (center_radius, shade, material: 48 B each)
-    // and the jitter table (stage_spp float2) to the start of the dynamic LDS and reads them
+    // and the jitter table (stage_spp float4) to the start of the dynamic LDS and reads them
     // there: the per-hit and per-sample reads leave global memory (L2 latency on every bounce).
     uint32_t stage_spheres, stage_spp;
 };
@@ -124,6 +128,15 @@ constexpr uint32_t kFlagRadiiSafe = 16u;  // every |radius| in [2^-40, 2^30] (ho
                                          // shading's (p - c) / r may take the unscaled division
 constexpr uint32_t kFlagDirect = 4u;  // one work item per pixel and frame, not progressive: the
                                       // lane writes the pixel itself (no sums, no resolve pass)
+
+// TraceParams.jitter from the host's jitter (vcrt_math.h rand2) and the camera: run at
+// vcrt_begin and for each progressive frame.
+struct SetupJitterParams {
+    const float2* jitter_in;  // [nsamples] (jx, jy)
+    float4* jitter;           // [nsamples] jx delta_u + jy delta_v
+    uint32_t nsamples;
+    float cam[12];  // as TraceParams.cam
+};
 
 // Exact sums -> pixels (vcrt_math.h resolve_channel), rgba32f with alpha 1.
 struct ResolveParams {
