@@ -66,6 +66,18 @@ __device__ __forceinline__ void tally_lds(uint32_t* slot, uint32_t x) {
 
 typedef __attribute__((address_space(4))) const float4 cfloat4;
 
+// A 32-bit constant materialized in a VGPR where it is used: the asm is volatile, so it is not
+// hoisted out of the persistent loop. Left to itself the compiler keeps constant pairs such as a
+// scan's initial (max_t, best) = (kInfinity, -1) live across the loop, and under the flat
+// kernel's register pressure spills them to scratch: a scratch load and a vmcnt wait per use.
+static_assert(__builtin_bit_cast(uint32_t, kInfinity) == 0x47c35000u, "vconst<kInfinity bits>");
+template <uint32_t kC>
+__device__ __forceinline__ uint32_t vconst() {
+    uint32_t r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "i"(kC));
+    return r;
+}
+
 // One group = four spheres in pair-SoA form: q[0] = (cx0,cx1,cy0,cy1), q[1] = (cz0,cz1,r0²,r1²),
 // q[2] = (cx2,cx3,cy2,cy3), q[3] = (cz2,cz3,r2²,r3²).
 struct Group {
@@ -1427,7 +1439,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         __syncthreads();
         tbound = lds_geom;
         tnode = lds_geom + nb;
-        ws = reinterpret_cast<WS*>(lds_geom + nb + nn) + (threadIdx.x >> 6);
+        ws = reinterpret_cast<WS*>(lds_geom + nb + nn) +
+             (threadIdx.x >> 6);
     }
     const uint32_t lane = threadIdx.x & 63u;
     const f3 p00 = mk(P.cam[0], P.cam[1], P.cam[2]);
@@ -1439,6 +1452,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     const bool chunk_minor = (P.flags & kFlagChunkMinor) != 0;
 
     bool done = false, need = true;
+    bool newray = false;  // the lane's next sample's camera ray is set up at the next fetch
     bool fin = false;  // the lane's quantum is finished and its sum in acc not yet added
     bool fresh = false;  // the lane's ray is a camera ray not yet traced (flat scan)
     // flat scan: a main-scan hit waits for the next iteration's shading (pend_t, pend_best;
@@ -1496,7 +1510,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     // Shades a traced segment (textures.glsl, or the sky of functions.glsl:85-89) and advances
     // the lane's path: accumulate and start the next sample's camera ray (returns true), or
     // finish the chunk (need), or continue with the bounced ray.
-    auto shade_and_advance = [&](float max_t, int best) -> bool {
+    // defer_ray: a sample that ends here leaves its next camera ray to the next iteration's fetch
+    // (which sets up new items' first rays anyway; used after the main scan, whose lanes trace
+    // that ray no earlier than the next camera fast trace)
+    auto shade_and_advance = [&](float max_t, int best, bool defer_ray) -> bool {
         bool ended = false, fresh_cam = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
         if (best >= 0) {
@@ -1584,11 +1601,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // a quantum of G samples ends inside the item: its sum is retired the same way,
                 // and the item goes on with its next sample
                 if (((uint32_t)sample & P.quantum_mask) == 0u) fin = true;
-                d = camera_dir(sample);
-                o = cam;
-                atten = mk(1.f, 1.f, 1.f);
-                pass = 0;
-                fresh_cam = true;
+                if (defer_ray) {
+                    newray = true;
+                } else {
+                    d = camera_dir(sample);
+                    o = cam;
+                    atten = mk(1.f, 1.f, 1.f);
+                    pass = 0;
+                    fresh_cam = true;
+                }
             }
         }
         return fresh_cam;
@@ -1645,6 +1666,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 }
             }
             acc = mk(0.f, 0.f, 0.f);  // the next quantum (of this item or the next) sums from 0
+        }
+        if (newray) {  // the next sample's camera ray (shader.comp:48-52), deferred by the sky
+            newray = false;
+            d = camera_dir(sample);
+            o = cam;
+            atten = mk(1.f, 1.f, 1.f);
+            pass = 0;
+            fresh = true;
         }
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
@@ -1796,8 +1825,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             const bool cam_now = fresh && (inf & 15u) != 15u && (P.flags & kFlagSceneBounded) != 0 &&
                                  aa >= 0x1p-20f && aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
-            float mt = kInfinity;
-            int bst = -1;
+            float mt = __uint_as_float(vconst<0x47c35000u>());  // kInfinity
+            int bst = (int)vconst<0xffffffffu>();                // -1
             if (__ballot(cam_now)) {
                 if constexpr (kStats) {
                     ++pt.cam_entries;
@@ -1877,7 +1906,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             }
             uint64_t t_cs = 0;
             if constexpr (kStats) t_cs = ticks();
-            if (cam_now || pending) fresh = shade_and_advance(mt, bst);
+            if (cam_now || pending) fresh = shade_and_advance(mt, bst, false);
             if constexpr (kStats) {
                 const uint64_t t1 = ticks();
                 pt.cam += t1 - t_cam;
@@ -1888,8 +1917,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 
         // ---- one segment: scan the whole sphere list (functions.glsl:73-81) ----
         ++segs;
-        float max_t = kInfinity;
-        int best = -1;
+        float max_t = __uint_as_float(vconst<0x47c35000u>());  // kInfinity
+        int best = (int)vconst<0xffffffffu>();                   // -1
         uint32_t hit_groups = 0;
         if constexpr (kCull != 0) {
             // culling needs every ray of the wave in the guarded finite range (see above)
@@ -1945,10 +1974,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 pend_best = best >= 0 ? best : kPendSky;
                 fresh = false;  // the ray is traced (it may have been a camera ray)
             } else {
-                fresh = shade_and_advance(max_t, best);  // the sky
+                fresh = shade_and_advance(max_t, best, true);  // the sky
             }
         } else {
-            fresh = shade_and_advance(max_t, best);
+            fresh = shade_and_advance(max_t, best, false);
         }
         if constexpr (kStats) pt.shade += ticks() - t_shade;
 
