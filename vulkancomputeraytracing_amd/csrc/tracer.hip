@@ -2269,7 +2269,14 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_check_sin(SinCheckParams 
         if (!ok) f = sin_canonical(x);
         fallback += ok ? 0u : 1u;
         const float want = sin_canonical(x);
-        if (__float_as_uint(f) != __float_as_uint(want)) {
+        // and the two-argument form the scatter uses (sin3: sin_fast_try_n<2>), on the input and
+        // its negation: every accepted value must be the canonical one
+        const float xs[2] = {x, -x};
+        float fs[2];
+        const bool ok2 = sin_fast_try_n<2>(xs, fs);
+        const bool bad2 = ok2 && (__float_as_uint(fs[0]) != __float_as_uint(want) ||
+                                  __float_as_uint(fs[1]) != __float_as_uint(sin_canonical(-x)));
+        if (__float_as_uint(f) != __float_as_uint(want) || bad2) {
             ++bad;
             first_bad = min(first_bad, bits);
         }
