@@ -1,3 +1,4 @@
 set -o pipefail
-bash tools/gpu_run.sh test || exit 1
-PREV=ab_objs/r3 OBJS="ab_objs/hoist.hsaco" AB_CFGS="c4 c2 c3 stress" ROUNDS=2 bash tools/gpu_run.sh ab || exit 1
+bash tools/gpu_run.sh test profile || exit 1
+SWEEP_REPS=1 WORLDS=2,4,8 bash tools/gpu_run.sh sweep || exit 1
+bash tools/gpu_run.sh phases || exit 1
