@@ -333,8 +333,7 @@ def test_work_chunk_rule(w, h, spp):
         assert k == spp or k % q == 0
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
         want = 64
-        floor = 32 if slots * -(-spp // 32) < (1 << 22) else 16  # small frames stop at 32
-        while want > floor and slots * -(-spp // want) < (1 << 24) - (1 << 21):
+        while want > 16 and slots * -(-spp // want) < (1 << 24) - (1 << 21):
             want //= 2
         assert k == min(_round_up(max(want, -(-spp // 512)), q), spp)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,

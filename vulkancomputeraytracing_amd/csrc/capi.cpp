@@ -143,19 +143,17 @@ RendererState g;
 // (profiles/r02_tail_sweep.txt, kernel ms per rank at the C4 workload): one GPU K = 64 127.0 /
 // K = 32 129.3 -> 64; 2-way shards 64.3 / 65.2 -> 64; 4-way K = 32 33.4 / K = 16 33.9 -> 32;
 // 8-way K = 16 17.6 / K = 32 17.7-18.1 -> 16; C3 (256 spp) K = 32 33.55 / K = 16 33.80 -> 32.
-// All ranks of a frame use the same K (the largest rank's share decides), so a sharded frame
-// equals a one-GPU render with that partition bit for bit.
-// Round 3: small frames (fewer than kSmallFrameItems items at K = 32) stop halving at 32: with
-// the accumulation ring an item's overhead is small but a latency-bound small frame still pays
-// it (C2, 800x450 x 64 spp: K = 32 1.35 ms against K = 16 1.47 ms).
+// All ranks of a frame use the same K (the largest rank's share decides); the image depends on
+// the accumulation quantum alone (work_quantum), whatever K and the tail are.
+// Round 3 stopped small frames (fewer than 2^22 items at K = 32) at K = 32, measured then at C2
+// (K = 32 1.35 ms against K = 16 1.47 ms, when the item was also the accumulation quantum and
+// every item end read its ring entry back). Round 4 dropped that floor: with the quantum
+// decoupled and the claim-time ring clearing, C2 takes 0.878-0.894 ms at K = 16 against
+// 0.936-0.959 at K = 32 (K = 8: 0.882-0.896; profiles/r04_ab_log.md).
 constexpr uint64_t kChunkItems = (uint64_t{1} << 24) - (uint64_t{1} << 21);
-constexpr uint64_t kSmallFrameItems = uint64_t{1} << 22;
-
 int32_t default_chunk(uint64_t rank_slots, int32_t spp) {
     int32_t k = kDefaultChunk;
-    const int32_t k_floor =
-        rank_slots * static_cast<uint64_t>((spp + 31) / 32) < kSmallFrameItems ? 32 : 16;
-    while (k > k_floor && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems)
+    while (k > 16 && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems)
         k /= 2;
     const int32_t k_min = (spp + vcrt::kAccumMaxChunks - 1) / vcrt::kAccumMaxChunks;
     return std::max(k, k_min);
