@@ -1084,6 +1084,7 @@ vcrt_result vcrt_draw_next_frame(void) {
                   (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
                   (g.direct ? vcrt::kFlagDirect : 0u);
         p.spp_total = static_cast<float>(spp_total);
+        for (int j = 0; j < 13; j++) p.sin_c[j] = vcrt::kSinC[j];
         const std::array<float, 12> cam = camera_array();
         for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
         const KernelChoice kc = select_kernel();
@@ -1378,7 +1379,9 @@ vcrt_result vcrt_selftest_sin(uint32_t first, uint32_t count, uint64_t* mismatch
     uint32_t init[6] = {0, 0, 0, 0, 0xFFFFFFFFu, 0};
     hipError_t e = hipMemcpy(buf, init, sizeof(init), hipMemcpyHostToDevice);
     vcrt::SinCheckParams sp{static_cast<unsigned long long*>(buf),
-                            reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + 16), first, count};
+                            reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + 16), first, count,
+                            {}};
+    for (int j = 0; j < 13; j++) sp.sin_c[j] = vcrt::kSinC[j];
     VkResult r = e == hipSuccess ? launch(f, 8 * 256 * 8, 256, 0, sp) : to_vk(e);
     uint32_t out[6] = {0, 0, 0, 0, 0, 0};
     if (r == VK_SUCCESS) {

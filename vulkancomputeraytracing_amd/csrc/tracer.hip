@@ -1538,8 +1538,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             // rand(dir.xy), rand(dir.xz), rand(dir.yz) for lambertian/metal (functions.glsl:43),
             // rand(point.xy) for glass (textures.glsl:51): three sines for every hit lane
             float s1, s2, s3;
-            sin3((type == 3) ? rand_arg(point.x, point.y) : rand_arg(d.x, d.y),
-                 rand_arg(d.x, d.z), rand_arg(d.y, d.z), s1, s2, s3);
+            sin3<true>((type == 3) ? rand_arg(point.x, point.y) : rand_arg(d.x, d.y),
+                       rand_arg(d.x, d.z), rand_arg(d.y, d.z), s1, s2, s3,
+                       (cdouble*)&P.sin_c[0]);
             const float r1 = rand_of_sin(s1);
             if (type == 1 || type == 2) {
                 const float r2 = rand_of_sin(s2);
@@ -2272,10 +2273,17 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_check_sin(SinCheckParams 
         // and the two-argument form the scatter uses (sin3: sin_fast_try_n<2>), on the input and
         // its negation: every accepted value must be the canonical one
         const float xs[2] = {x, -x};
-        float fs[2];
+        float fs[2], ft[2], fu[1];
         const bool ok2 = sin_fast_try_n<2>(xs, fs);
-        const bool bad2 = ok2 && (__float_as_uint(fs[0]) != __float_as_uint(want) ||
-                                  __float_as_uint(fs[1]) != __float_as_uint(sin_canonical(-x)));
+        // and the table form (constants from the kernel arguments, as the tracer reads them)
+        const bool okt = sin_fast_try_n<2, true>(xs, ft, (cdouble*)&p.sin_c[0]);
+        const bool oku = sin_fast_try_n<1, true>(xs, fu, (cdouble*)&p.sin_c[0]);
+        const float wneg = sin_canonical(-x);
+        const bool bad2 = (ok2 && (__float_as_uint(fs[0]) != __float_as_uint(want) ||
+                                   __float_as_uint(fs[1]) != __float_as_uint(wneg))) ||
+                          (okt && (__float_as_uint(ft[0]) != __float_as_uint(want) ||
+                                   __float_as_uint(ft[1]) != __float_as_uint(wneg))) ||
+                          (oku && __float_as_uint(fu[0]) != __float_as_uint(want));
         if (__float_as_uint(f) != __float_as_uint(want) || bad2) {
             ++bad;
             first_bad = min(first_bad, bits);

@@ -98,6 +98,7 @@ struct TraceParams {
     // and the jitter table (stage_spp float4) to the start of the dynamic LDS and reads them
     // there: the per-hit and per-sample reads leave global memory (L2 latency on every bounce).
     uint32_t stage_spheres, stage_spp;
+    double sin_c[13];  // vcrt_math.h kSinC: the fast sine's constants, read by scalar loads
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
@@ -166,6 +167,7 @@ struct SinCheckParams {
     unsigned long long* result;  // [2]: inputs where sin_fast != sin_canonical, fallbacks
     uint32_t* first_bad;         // smallest differing bit pattern (init 0xFFFFFFFF)
     uint32_t first, count;       // input bit patterns first .. first + count - 1
+    double sin_c[13];            // vcrt_math.h kSinC, for the table form the tracer uses
 };
 
 struct FillParams {

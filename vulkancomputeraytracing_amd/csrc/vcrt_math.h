@@ -205,6 +205,16 @@ VCRT_HD float sin_canonical(float xf) {
     return (float)s;
 }
 
+// The fast sine's constants in the order sin_fast_try_n reads them from a table (kTab): 1/pi,
+// the 1.5 * 2^52 shifter, pi_hi, pi_mid, then (-1)^j / (2j+1)! for j = 9 .. 1. The host copies
+// them into TraceParams.sin_c; the literals in sin_fast_try_n are the same values.
+constexpr double kSinC[13] = {0.31830988618379067154, 0x1.8p52, 0x1.921fb544p+1,
+                              0x1.0b4611a626331p-33, -0x1.2f49b46814157p-57,
+                              0x1.952c77030ad4ap-49, -0x1.ae7f3e733b81fp-41,
+                              0x1.6124613a86d09p-33, -0x1.ae64567f544e4p-26,
+                              0x1.71de3a556c734p-19, -0x1.a01a01a01a01ap-13,
+                              0x1.1111111111111p-7, -0x1.5555555555555p-3};
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // The canonical sin on the device, by Ziv's method: one branch-free evaluation for every lane
 // (sin_canonical evaluates both fdlibm kernels under divergence, since the quadrant varies per
@@ -274,42 +284,52 @@ __device__ __forceinline__ bool sin_fast_try(float xf, float& out) {
 // sin_fast_try of N arguments at once, step by step: each constant is materialized once and
 // used by the N evaluations (sconst's two s_mov_b32 per use were ~90 SALU instructions per
 // scatter with three separate calls), each argument's operations unchanged.
-template <int N>
-__device__ __forceinline__ bool sin_fast_try_n(const float* xf, float* out) {
+typedef __attribute__((address_space(4))) const double cdouble;
+template <int N, bool kTab = false>
+__device__ __forceinline__ bool sin_fast_try_n(const float* xf, float* out,
+                                               cdouble* kc = nullptr) {
+#define VCRT_SC(j, lit)                                 \
+    ([&]() -> double {                                  \
+        if constexpr (kTab)                             \
+            return kc[j];                               \
+        else                                            \
+            return VCRT_DC(lit);                        \
+    }())
     double x[N], t[N], k[N], r[N], r2[N], p[N];
     for (int i = 0; i < N; ++i) x[i] = (double)xf[i];
     {
-        const double c = VCRT_DC(0.31830988618379067154), sh = VCRT_DC(0x1.8p52);
+        const double c = VCRT_SC(0, 0.31830988618379067154), sh = VCRT_SC(1, 0x1.8p52);
         for (int i = 0; i < N; ++i) t[i] = __builtin_fma(x[i], c, sh);
         for (int i = 0; i < N; ++i) k[i] = t[i] - sh;
     }
     {
-        const double c = VCRT_DC(0x1.921fb544p+1);
+        const double c = VCRT_SC(2, 0x1.921fb544p+1);
         for (int i = 0; i < N; ++i) r[i] = __builtin_fma(-k[i], c, x[i]);
     }
     {
-        const double c = VCRT_DC(0x1.0b4611a626331p-33);
+        const double c = VCRT_SC(3, 0x1.0b4611a626331p-33);
         for (int i = 0; i < N; ++i) r[i] = __builtin_fma(-k[i], c, r[i]);
     }
     for (int i = 0; i < N; ++i) r2[i] = r[i] * r[i];
     {
-        const double c = VCRT_DC(-0x1.2f49b46814157p-57);  // (-1)^j / (2j+1)!, j = 9 .. 1
+        const double c = VCRT_SC(4, -0x1.2f49b46814157p-57);  // (-1)^j / (2j+1)!, j = 9 .. 1
         for (int i = 0; i < N; ++i) p[i] = c;
     }
-#define VCRT_SIN3_STEP(C)                                                  \
+#define VCRT_SIN3_STEP(J, C)                                               \
     {                                                                      \
-        const double c = VCRT_DC(C);                                       \
+        const double c = VCRT_SC(J, C);                                    \
         for (int i = 0; i < N; ++i) p[i] = fma_vvs(p[i], r2[i], c);        \
     }
-    VCRT_SIN3_STEP(0x1.952c77030ad4ap-49)
-    VCRT_SIN3_STEP(-0x1.ae7f3e733b81fp-41)
-    VCRT_SIN3_STEP(0x1.6124613a86d09p-33)
-    VCRT_SIN3_STEP(-0x1.ae64567f544e4p-26)
-    VCRT_SIN3_STEP(0x1.71de3a556c734p-19)
-    VCRT_SIN3_STEP(-0x1.a01a01a01a01ap-13)
-    VCRT_SIN3_STEP(0x1.1111111111111p-7)
-    VCRT_SIN3_STEP(-0x1.5555555555555p-3)
+    VCRT_SIN3_STEP(5, 0x1.952c77030ad4ap-49)
+    VCRT_SIN3_STEP(6, -0x1.ae7f3e733b81fp-41)
+    VCRT_SIN3_STEP(7, 0x1.6124613a86d09p-33)
+    VCRT_SIN3_STEP(8, -0x1.ae64567f544e4p-26)
+    VCRT_SIN3_STEP(9, 0x1.71de3a556c734p-19)
+    VCRT_SIN3_STEP(10, -0x1.a01a01a01a01ap-13)
+    VCRT_SIN3_STEP(11, 0x1.1111111111111p-7)
+    VCRT_SIN3_STEP(12, -0x1.5555555555555p-3)
 #undef VCRT_SIN3_STEP
+#undef VCRT_SC
     bool ok = true;
     for (int i = 0; i < N; ++i) {
         const double s = __builtin_fma(r[i] * r2[i], p[i], r[i]);
@@ -328,11 +348,20 @@ __device__ __forceinline__ bool sin_fast_try_n(const float* xf, float* out) {
 // three separate calls; all three interleaved spilled a loop counter), a3 by sin_fast_try; a
 // lane whose fast values were not all accepted recomputes all three
 // canonically in one loop (one inlined copy of the fdlibm path instead of three).
+template <bool kTab = false>
 __device__ __forceinline__ void sin3(float a1, float a2, float a3, float& s1, float& s2,
-                                     float& s3) {
+                                     float& s3, cdouble* kc = nullptr) {
     const float a[2] = {a1, a2};
     float sv[2];
-    const bool ok = sin_fast_try_n<2>(a, sv) & sin_fast_try(a3, s3);
+    bool ok = sin_fast_try_n<2, kTab>(a, sv, kc);
+    if constexpr (kTab) {
+        const float a3v[1] = {a3};
+        float s3v[1];
+        ok = ok & sin_fast_try_n<1, true>(a3v, s3v, kc);
+        s3 = s3v[0];
+    } else {
+        ok = ok & sin_fast_try(a3, s3);
+    }
     s1 = sv[0];
     s2 = sv[1];
     if (!ok) {
