@@ -346,10 +346,14 @@ __device__ __forceinline__ void pair_disc_cam(const v2f dx, const v2f dy, const 
 }
 
 __device__ __forceinline__ void consider(float t, int idx, float& max_t, int& best) {
-    if (t > kMinT && (t < max_t || (t == max_t && best >= 0 && idx < best))) {
-        max_t = t;
-        best = idx;
-    }
+    // (t, idx) < (max_t, best) lexicographically, as one 64-bit compare of (bits(t), index)
+    // (t, max_t > min_t > 0 order as their bits); best < 0 (none yet) counts as index 0, so a
+    // t equal to the initial max_t is never taken, as in hit_sphere's strict "<"
+    const uint64_t kt = ((uint64_t)__float_as_uint(t) << 32) | (uint32_t)idx;
+    const uint64_t km = ((uint64_t)__float_as_uint(max_t) << 32) | (uint32_t)max(best, 0);
+    const bool take = (t > kMinT) & (kt < km);
+    max_t = take ? t : max_t;
+    best = take ? idx : best;
 }
 
 __device__ __forceinline__ v2f vfma(v2f x, v2f y, v2f z) {
