@@ -292,18 +292,20 @@ __device__ __forceinline__ float sqrt_unscaled(float x) {
 // for lanes outside [2^-96, inf] (tiny, zero, negative or NaN x).
 __device__ __forceinline__ float sqrt_fast(float x) {
     float r = sqrt_unscaled(x);
-    if (!(x >= 0x1p-96f)) {
+    if (__ballot(!(x >= 0x1p-96f))) {  // wave-uniform: no exec-mask save and restore
         asm volatile("");
-        r = __builtin_sqrtf(x);
+        const float full = __builtin_sqrtf(x);
+        r = !(x >= 0x1p-96f) ? full : r;
     }
     return r;
 }
 
 __device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a, float ya) {
     float sq = sqrt_unscaled(disc);
-    if (disc < 0x1p-96f) {
+    if (__ballot(disc < 0x1p-96f)) {  // wave-uniform: no exec-mask save and restore
         asm volatile("");  // a real branch: hipcc would otherwise run the full sqrt for every lane
-        sq = __builtin_sqrtf(disc);
+        const float full = __builtin_sqrtf(disc);
+        sq = disc < 0x1p-96f ? full : sq;
     }
     const float r1 = div_a(-hb - sq, a, ya);
     if (r1 > kMinT) return r1;
