@@ -100,7 +100,8 @@ def marker_lines():
     m["shade"] = find("// ---- shade (textures.glsl)", m["scan"])
     m["end"] = find("VCRT_WAVE_END_TIMES", m["shade"])
     # the real branches of the rare fallbacks (asm volatile(""): not if-converted)
-    m["rare"] = {find("r = __builtin_sqrtf(x);"), find("sq = __builtin_sqrtf(disc);"),
+    m["rare"] = {find("const float full = __builtin_sqrtf(x);"),
+                 find("const float full = __builtin_sqrtf(disc);"),
                  find("normal = divs(pcv, cr.w);")}
     return m
 
