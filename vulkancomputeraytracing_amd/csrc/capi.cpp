@@ -105,6 +105,7 @@ struct RendererState {
     // per-frame inputs / outputs
     float2* d_jitter_in = nullptr;  // the host's jitter (jx, jy) of the frame's sample indices
     float4* d_jitter = nullptr;     // TraceParams.jitter (vcrt_setup_jitter)
+    float4* d_corner = nullptr;     // TraceParams.corner (vcrt_setup_jitter, at vcrt_begin)
     float4* d_fb_own = nullptr;
     float4* d_fb = nullptr;  // current render target (own or caller-provided)
     size_t fb_bytes = 0;
@@ -448,7 +449,7 @@ VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Pa
 // TraceParams.jitter (vcrt_kernel_abi.h SetupJitterParams): the jitter term of the frame's
 // sample indices base .. base + spp - 1 (shader.comp:48), on the device with the tracer's own
 // operations.
-VkResult setup_jitter(uint64_t base) {
+VkResult setup_jitter(uint64_t base, bool corners = false) {
     const int spp = g.desc.samples_per_pixel;
     make_jitter(base, spp, g.jitter_host);
     VCRT_TRY(hipMemcpyAsync(g.d_jitter_in, g.jitter_host.data(), sizeof(float2) * spp,
@@ -459,7 +460,13 @@ VkResult setup_jitter(uint64_t base) {
     sp.nsamples = static_cast<uint32_t>(spp);
     const std::array<float, 12> cam = camera_array();
     for (int i = 0; i < 12; i++) sp.cam[i] = cam[i];
-    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((spp + 255) / 256, 1024));
+    sp.corner = corners ? g.d_corner : nullptr;
+    sp.slots = g.total_pixels;
+    sp.tiles_x = g.tiles_x;
+    sp.rank = static_cast<uint32_t>(g.desc.rank);
+    sp.world = static_cast<uint32_t>(g.desc.world_size);
+    const uint64_t total = static_cast<uint64_t>(spp) + (sp.corner ? sp.slots : 0u);
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((total + 255) / 256, 8192));
     VkResult r = launch(g.k_setup_jitter, grid, 256, 0, sp);
     if (r != VK_SUCCESS) return r;
     VCRT_TRY(hipStreamSynchronize(g.stream));  // jitter_host is reused by the next frame
@@ -762,7 +769,6 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     const int spp = g.desc.samples_per_pixel;
     if ((r = to_vk(hipMalloc(&g.d_jitter_in, sizeof(float2) * spp))) != VK_SUCCESS) return fail(r);
     if ((r = to_vk(hipMalloc(&g.d_jitter, sizeof(float4) * spp))) != VK_SUCCESS) return fail(r);
-    if ((r = setup_jitter(0)) != VK_SUCCESS) return fail(r);
     {
         float th[255];
         srgb_thresholds(th);
@@ -799,6 +805,11 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     // Work decomposition: (local tile, chunk of K samples) items holding whole quanta; a pixel's
     // quantum sums are combined exactly (vcrt_math.h "Accumulation"), at most kAccumMaxChunks.
     g.total_pixels = g.local_tiles * 64u;  // local element slots incl. partial-tile padding
+    // the camera-ray tables: the jitter terms and the local slots' pixel corners
+    if (g.total_pixels &&
+        (r = to_vk(hipMalloc(&g.d_corner, sizeof(float4) * g.total_pixels))) != VK_SUCCESS)
+        return fail(r);
+    if ((r = setup_jitter(0, g.total_pixels != 0)) != VK_SUCCESS) return fail(r);
     g.quantum = work_quantum(g.desc);
     if ((spp + g.quantum - 1) / g.quantum > vcrt::kAccumMaxChunks)
         return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
@@ -1045,6 +1056,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.shade = g.d_shade;
         p.material = g.d_material;
         p.jitter = g.d_jitter;
+        p.corner = g.d_corner;
         p.out = g.d_fb;
         p.accum = g.d_accum;
         p.work = reinterpret_cast<uint32_t*>(static_cast<char*>(g.d_counters) + 256);
@@ -1229,6 +1241,7 @@ vcrt_result vcrt_end(void) {
     free_scene();
     if (g.d_jitter) (void)hipFree(g.d_jitter);
     if (g.d_jitter_in) (void)hipFree(g.d_jitter_in);
+    if (g.d_corner) (void)hipFree(g.d_corner);
     if (g.d_fb_own) (void)hipFree(g.d_fb_own);
     if (g.d_counters) (void)hipFree(g.d_counters);
     if (g.d_debug) (void)hipFree(g.d_debug);

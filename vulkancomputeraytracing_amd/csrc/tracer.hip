@@ -1470,12 +1470,18 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     uint32_t pxy = 0;  // the item's pixel: y << 16 | x
     f3 o = mk(0.f, 0.f, 0.f), d = o, atten = o, acc = o;
     // shader.comp:43-52: the camera ray of sample s of the lane's pixel, (corner + jitter) - center,
-    // the jitter term from its table (the same operations, done once per sample index instead of
-    // at every sample start; a table of the pixel corners as well measured no faster: its loads
-    // cost what its VALU savings gained). The corner is recomputed from pxy (three VGPRs fewer
-    // across the loop than keeping it).
+    // both terms from tables built with the same operations (TraceParams.jitter per sample index,
+    // TraceParams.corner per local slot) instead of 25 VALU instructions at every sample start:
+    // C4 +1.1%, C3 +1.1% (profiles/r04_ab_log.md). The linear scans (C2: a small, latency-bound
+    // frame, -6% with the corner's load) recompute the corner from pxy.
     auto camera_dir = [&](int s) {
-        const f3 c = viewport_corner(p00, du, dv, pxy & 0xffffu, pxy >> 16);
+        f3 c;
+        if constexpr (kCull != 0) {  // the culled scans: the corner from its table
+            const float4 c4 = P.corner[q & kQMask];
+            c = mk(c4.x, c4.y, c4.z);
+        } else {  // the linear scans (small, latency-bound frames): computed, no load
+            c = viewport_corner(p00, du, dv, pxy & 0xffffu, pxy >> 16);
+        }
         const float4 j = jitter_at<kStageable>(P, lds_dyn, s);
         return sub(add(c, mk(j.x, j.y, j.z)), cam);
     };
@@ -2213,12 +2219,22 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) 
 
 // TraceParams.jitter (SetupJitterParams): the jitter term of every sample index.
 extern "C" __global__ __launch_bounds__(256) void vcrt_setup_jitter(SetupJitterParams p) {
+    const f3 p00 = mk(p.cam[0], p.cam[1], p.cam[2]);
     const f3 du = mk(p.cam[3], p.cam[4], p.cam[5]);
     const f3 dv = mk(p.cam[6], p.cam[7], p.cam[8]);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.nsamples;
+    const uint32_t total = p.nsamples + (p.corner ? p.slots : 0u);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += gridDim.x * blockDim.x) {
-        const f3 v = viewport_jitter(du, dv, p.jitter_in[i]);
-        p.jitter[i] = make_float4(v.x, v.y, v.z, 0.0f);
+        if (i < p.nsamples) {
+            const f3 v = viewport_jitter(du, dv, p.jitter_in[i]);
+            p.jitter[i] = make_float4(v.x, v.y, v.z, 0.0f);
+        } else {  // the pixel corner of local slot q (edge-tile slots outside the frame too)
+            const uint32_t q = i - p.nsamples, slot = q & 63u;
+            uint32_t tx, ty;
+            tile_of(q >> 6, p.rank, p.world, p.tiles_x, &tx, &ty);
+            const f3 c = viewport_corner(p00, du, dv, 8u * tx + (slot & 7u), 8u * ty + (slot >> 3));
+            p.corner[q] = make_float4(c.x, c.y, c.z, 0.0f);
+        }
     }
 }
 

@@ -99,6 +99,8 @@ struct TraceParams {
     // there: the per-hit and per-sample reads leave global memory (L2 latency on every bounce).
     uint32_t stage_spheres, stage_spp;
     double sin_c[13];  // vcrt_math.h kSinC: the fast sine's constants, read by scalar loads
+    const float4* corner;  // [local_tiles * 64] pixel00 + x delta_u + y delta_v per local slot
+                           //   (shader.comp:43; vcrt_setup_jitter, the kernel's own operations)
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
@@ -137,6 +139,8 @@ struct SetupJitterParams {
     float4* jitter;           // [nsamples] jx delta_u + jy delta_v
     uint32_t nsamples;
     float cam[12];  // as TraceParams.cam
+    float4* corner;  // [slots] the local slots' pixel corners, or null
+    uint32_t slots, tiles_x, rank, world;
 };
 
 // Exact sums -> pixels (vcrt_math.h resolve_channel), rgba32f with alpha 1.
