@@ -26,8 +26,9 @@ struct TraceParams {
     const float4* material;       // [n] (texture.x = material id, 1 / texture.y, Schlick r0^2
                                   //   of texture.y, 0): the glass quotients precomputed (fp32)
     // shader.comp:43-49's viewport point pixel00 + x delta_u + y delta_v + jx delta_u + jy delta_v
-    // is the sum of two fp32 terms: the pixel's corner (computed at each sample start) and the
-    // sample's jitter term, a table (vcrt_setup_jitter, the kernel's own operations)
+    // is the sum of two fp32 terms: the pixel's corner (the `corner` table below for the culled
+    // scans, computed at each sample start by the linear ones) and the sample's jitter term, a
+    // table (vcrt_setup_jitter, the kernel's own operations)
     const float4* jitter;  // [spp] jx delta_u + jy delta_v, (jx, jy) = (-0.5+rand(i,i),
                            //   -0.5+rand(i+1,i+1)) of sample index i (shader.comp:48)
     float4* out;           // rank-local framebuffer, rgba32f (layout above)
