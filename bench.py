@@ -63,12 +63,15 @@ def parse():
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--validate", action="store_true",
-                   help="after the timed steps, rank 0 checks its frame: bit for bit against the "
-                        "CPU oracle on a few rows at full spp, and (N > 1) against a 1-GPU "
-                        "render of the whole frame. Always on when N > 1 (the multi-GPU line "
-                        "proves its own gather); --no-validate turns it off")
+                   help="(the default) after the timed steps, rank 0 checks its frame: bit for "
+                        "bit against the CPU oracle on pixels of a few full-width rows at full "
+                        "spp and depth, and (N > 1) against a 1-GPU render of the whole frame; "
+                        "--no-validate turns it off")
     p.add_argument("--no-validate", action="store_true")
     p.add_argument("--validate-rows", type=int, default=2)
+    p.add_argument("--validate-budget", type=float, default=1e10,
+                   help="oracle sphere tests the row check may cost (~2 s on 16 threads): wider "
+                        "or deeper workloads check every k-th pixel of the rows")
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="target CPU work for the cpu_baseline sample")
     a = p.parse_args()
@@ -167,9 +170,11 @@ def cpu_baseline(args):
 # ---- validation (outside the timed region) ---------------------------------------------------
 
 def validate(args, got, st, device, world):
-    """Rank 0's frame against the CPU oracle on a few full-width rows at full spp and depth
-    (bit for bit, same accumulation quantum), and for N > 1 against a default 1-GPU render of
-    the whole frame: the image depends on the quantum alone, which does not depend on N."""
+    """Rank 0's frame against the CPU oracle on the pixels of a few full-width rows at full spp
+    and depth (bit for bit, same accumulation quantum and scale; every k-th pixel of the rows when
+    the whole rows would cost the oracle more than --validate-budget sphere tests), and for N > 1
+    against a default 1-GPU render of the whole frame: the image depends on the quantum and the
+    scene's scale alone, neither of which depends on N. Runs outside the timed region."""
     import numpy as np
     from tests import oracle_py
     import vulkancomputeraytracing_amd as vc
@@ -177,12 +182,22 @@ def validate(args, got, st, device, world):
     out = {}
     rows = list(range(args.height // (2 * args.validate_rows), args.height,
                       max(1, args.height // args.validate_rows)))[:args.validate_rows]
+    scene = o.scene(args.scene)
+    # ~4 segments per sample on the reference scenes' mix of sky, ground and spheres
+    per_pixel = float(args.spp) * 4.0 * len(scene)
+    stride = max(1, int(np.ceil(len(rows) * args.width * per_pixel / args.validate_budget)))
+    xy = np.array([(x, y) for y in rows for x in range(stride // 2, args.width, stride)],
+                  dtype=np.int32)
     cfg = o.config(args.width, args.height, args.spp, args.depth, **o.partition(st))
-    want = np.stack([o.render(cfg, o.scene(args.scene), rows=range(y, y + 1), threads=cpu_quota())[0][y]
-                     for y in rows])
+    t0 = time.perf_counter()
+    want, _ = o.render_pixels(cfg, scene, xy, threads=cpu_quota())
     out["rows_vs_oracle"] = rows
-    out["bitwise_vs_oracle"] = bool(np.array_equal(got[rows].view(np.uint32),
+    out["pixels_vs_oracle"] = int(len(xy))
+    out["pixel_stride"] = stride
+    out["oracle_seconds"] = round(time.perf_counter() - t0, 2)
+    out["bitwise_vs_oracle"] = bool(np.array_equal(got[xy[:, 1], xy[:, 0]].view(np.uint32),
                                                    want.view(np.uint32)))
+    out["accumulate_scale_log2"] = st["accumulate_scale_log2"]
     if world > 1:
         # the default 1-GPU frame (its own work items): equal bit for bit when the gather is right
         ref_desc = vc.RenderDesc(width=args.width, height=args.height, samples_per_pixel=args.spp,
@@ -299,7 +314,8 @@ def main():
     if world > 1:
         rank_ms = [None] * world
         dist.all_gather_object(rank_ms, k_mean)
-    do_validate = (args.validate or world > 1) and not args.no_validate
+    # every line proves its own frame (outside the timed region) unless --no-validate
+    do_validate = not args.no_validate
     got = None
     if do_validate and rank == 0:  # a host copy, before the renderer closes
         got = frame.cpu().numpy() if frame is not None else r.read_framebuffer()

@@ -117,8 +117,9 @@ typedef struct vcrt_render_desc {
                                    at every progressive frame); when one quantum covers the pixel
                                    (G >= samples_per_pixel, not progressive) the sum is divided in
                                    fp32, the reference's sequential sum (shader.comp:46-56)
-                                   exactly; otherwise every quantum sum is quantized to 2^-32 and
-                                   added exactly. So the image depends on G only -- not on the
+                                   exactly; otherwise every quantum sum is quantized to 2^-s (s:
+                                   vcrt_work_scale, 32 for the reference scenes) and added
+                                   exactly. So the image depends on G (and the scene's s) only -- not on the
                                    work items, the schedule or the number of GPUs: a sharded frame
                                    equals a one-GPU render bit for bit. Work items hold whole
                                    quanta. At most 512 quanta per pixel (progressive frames
@@ -145,7 +146,7 @@ typedef struct vcrt_stats {
     uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
     uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */
     char kernel[48];       /* the tracer kernel the last frame launched (its code-object symbol) */
-    uint64_t debug[32]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
+    uint64_t debug[64]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
                            active-lane sum, hit groups, fetches, last/first wave end time, sum
                            end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,
                            its uniform levels, node / group / candidate passes (CULL_FLAT),
@@ -154,12 +155,18 @@ typedef struct vcrt_stats {
                            entries dealt, live lanes offered, partial passes, passes; [23]
                            the camera fast trace with its shading; [24..31] camera fast
                            trace entries, its lanes, live lanes, listed-group loop trips and
-                           lane sum, root loop trips and lane sum; main-scan hit lanes */
+                           lane sum, root loop trips and lane sum; main-scan hit lanes;
+                           [32..39] flat scans: wave ticks in the retire, wave-iterations
+                           running the fetch loop, block fetches, items started, next items
+                           handed out, item switches in the shading, wave-iterations running
+                           the retire, quanta retired (lanes); [40..63] region counters */
     int32_t accumulate_tail;       /* tail samples per pixel in effect (0: none) */
     int32_t accumulate_tail_chunk; /* samples per tail item in effect */
     int32_t ring_entries;          /* LDS accumulation ring entries per wave (0: none; the chunk
                                       sums go to global memory directly) */
     int32_t accumulate_quantum;    /* the accumulation quantum G in effect */
+    int32_t accumulate_scale_log2; /* s of the quantization scale 2^s of the quantum sums (per
+                                      scene: vcrt_work_scale) */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
@@ -180,6 +187,14 @@ int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
  * The head ends on a quantum boundary (T is adjusted) and tail items are rounded up to whole
  * quanta. Negative VkResult for an invalid desc. */
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
+/* The quantization scale 2^s of the quantum sums for a scene under desc (host only): the
+ * largest s <= 32 with G * R * 2^s < 2^44, where G is the quantum and R = A^max_depth bounds one
+ * sample's radiance, A the scene's largest per-bounce attenuation (Lambertian albedo * param,
+ * metal albedo; at least 1). So every finite quantum sum is held exactly, whatever the scene;
+ * the reference scenes take s = 32. One quantum per pixel: 32 (no quantization). Returns
+ * VCRT_ERROR_FORMAT_NOT_SUPPORTED when no scale holds the scene (R > 2^120). */
+vcrt_result vcrt_work_scale(const vcrt_render_desc* desc, const vcrt_sphere* spheres,
+                            int32_t count, int32_t* scale_log2);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
  * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final
  * scene at 1080p, ~0.4 s for 4100 spheres at 4K). vcrt_begin sets the final scene. */

@@ -343,7 +343,40 @@ typedef struct {
     volatile int next; /* row (or pixel-batch) counter */
     pthread_mutex_t lock;
     uint64_t segments;
+    int32_t scale_log2; /* the quantization scale 2^s of the quantum sums (oracle_scale_log2) */
 } render_job;
+
+/* The quantization scale 2^s of the quantum sums (vulkancomputeraytracing_amd/csrc/vcrt_math.h
+ * "Accumulation", restated from the rule, not shared code): one sample's radiance is the sky's
+ * factor (functions.glsl:86-88, <= 1) times the attenuation of each bounce -- albedo * param for
+ * Lambertian (textures.glsl:22), albedo for metal (:60), 1 for glass (:27-56) -- so its magnitude
+ * is at most R = A^depth, A = max(1, the scene's largest factor). A run of G samples sums to at
+ * most G R; s is the largest integer <= 32 with G R 2^s < 2^44 (slack factors for the fp32
+ * roundings: two per bounce, the sky's mix, the run's additions). Material ids convert like the
+ * kernel's (int) of texture.x; ids out of int range (or NaN) count as both Lambertian and metal;
+ * non-finite factors are left out (they only make radiance non-finite: a NaN pixel). Returns
+ * INT32_MIN when no s >= -80 holds the scene. */
+int32_t oracle_scale_log2(const oracle_sphere* world, int32_t n, int32_t max_depth,
+                          int32_t quantum) {
+    double a = 1.0;
+    for (int32_t i = 0; i < n; i++) {
+        const float id = world[i].texture[0];
+        const int known = fabsf(id) < 2147483648.0f;
+        const int t = known ? (int)id : 0;
+        for (int c = 0; c < 3; c++) {
+            const double col = fabs((double)world[i].colour[c]);
+            const double f = col * fabs((double)world[i].texture[1]);
+            if ((!known || t == 1) && isfinite(f) && f > a) a = f;
+            if ((!known || t == 2) && isfinite(col) && col > a) a = col;
+        }
+    }
+    const double r = pow(a * (1.0 + 0x1p-22), max_depth > 1 ? max_depth : 1) * (1.0 + 0x1p-20) *
+                     (double)quantum * (1.0 + (double)quantum * 0x1p-23);
+    if (!(r < 0x1p120)) return INT32_MIN;
+    int32_t sc = 32;
+    while (sc > -80 && ldexp(r, sc) >= 0x1p44) sc--;
+    return ldexp(r, sc) < 0x1p44 ? sc : INT32_MIN;
+}
 
 /* One pixel (shader.comp:43-57) into px[4]. Accumulation (vulkancomputeraytracing_amd/csrc/
  * vcrt_math.h "Accumulation"): the samples are cut into quanta of G (accumulate_quantum; before
@@ -351,9 +384,10 @@ typedef struct {
  * progressive frame of frame_spp samples; a quantum is summed in fp32 in sample order, as the
  * reference sums (shader.comp:46-54). A single chunk (K >= spp, no progressive frames) is then
  * divided by SAMPLES_PER_PIXEL in fp32: the reference's own arithmetic (shader.comp:56).
- * Otherwise every chunk sum S is quantized to q = RN_even(S * 2^32) (|S| < 2^12; a NaN, infinite
- * or larger sum makes the pixel NaN), the q are added exactly (integers below 2^53 in double),
- * and the pixel is (float)((sum * 2^-32) / spp). */
+ * Otherwise every quantum sum S is quantized to q = RN_even(S * 2^s) with the scene's scale
+ * (oracle_scale_log2; |S * 2^s| < 2^44, a NaN, infinite or larger scaled sum makes the pixel
+ * NaN), the q are added exactly (integers below 2^53 in double), and the pixel is
+ * (float)((sum * 2^-s) / spp). */
 static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* segs) {
     const oracle_config* cfg = job->cfg;
     v3 p00 = V(job->cam[0], job->cam[1], job->cam[2]);
@@ -401,13 +435,14 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
             v3 dir = vsub(ps, center);
             part = vadd(part, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
         }
-        const float m = fmaxf(fmaxf(fabsf(part.x), fabsf(part.y)), fabsf(part.z));
-        if (isnan(part.x) || isnan(part.y) || isnan(part.z) || !(m < 4096.0f)) {
-            sum[0] = sum[1] = sum[2] = NAN;
+        const float sc = ldexpf(1.0f, job->scale_log2);
+        const float qx = part.x * sc, qy = part.y * sc, qz = part.z * sc;
+        if (!(fabsf(qx) < 0x1p44f && fabsf(qy) < 0x1p44f && fabsf(qz) < 0x1p44f)) {
+            sum[0] = sum[1] = sum[2] = NAN; /* NaN stays NaN through later additions */
         } else {
-            sum[0] += (double)rintf(part.x * 0x1p32f);
-            sum[1] += (double)rintf(part.y * 0x1p32f);
-            sum[2] += (double)rintf(part.z * 0x1p32f);
+            sum[0] += (double)rintf(qx);
+            sum[1] += (double)rintf(qy);
+            sum[2] += (double)rintf(qz);
         }
         c0 = c1;
     }
@@ -416,7 +451,8 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
         px[1] = part.y / (float)cfg->spp;
         px[2] = part.z / (float)cfg->spp;
     } else {
-        for (int k = 0; k < 3; k++) px[k] = (float)((sum[k] * 0x1p-32) / (double)cfg->spp);
+        for (int k = 0; k < 3; k++)
+            px[k] = (float)((sum[k] * ldexp(1.0, -job->scale_log2)) / (double)cfg->spp);
     }
     px[3] = 1.0f;
 }
@@ -448,8 +484,21 @@ static void* render_worker(void* arg) {
     return NULL;
 }
 
+/* The longest run of samples summed in fp32 before quantization (the G of oracle_scale_log2). */
+static int32_t run_length(const oracle_config* cfg) {
+    if (cfg->accumulate_quantum > 0) return cfg->accumulate_quantum;
+    const int32_t block = (cfg->frame_spp <= 0 || cfg->frame_spp > cfg->spp) ? cfg->spp
+                                                                            : cfg->frame_spp;
+    int32_t g = (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block)
+                    ? block : cfg->accumulate_chunk;
+    if (cfg->accumulate_tail_chunk > g) g = cfg->accumulate_tail_chunk;
+    return g;
+}
+
 static int run_job(render_job* job, int32_t threads, uint64_t* segments) {
     const oracle_config* cfg = job->cfg;
+    job->scale_log2 = oracle_scale_log2(job->world, job->n, cfg->max_depth, run_length(cfg));
+    if (job->scale_log2 == INT32_MIN) return -1;
     oracle_camera(cfg, job->cam);
     float* jit = (float*)malloc(sizeof(float) * 2 * (size_t)cfg->spp);
     if (!jit) return -1;

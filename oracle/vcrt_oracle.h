@@ -77,6 +77,12 @@ int oracle_render_pixels(const oracle_config* cfg, const oracle_sphere* world, i
                          const int32_t* xy, int32_t npixels, float* rgba, int32_t threads,
                          uint64_t* segments);
 
+/* The quantization scale 2^s of the quantum sums for a scene, depth and quantum G (the largest
+ * s <= 32 with G * A^depth * 2^s < 2^44, A the largest per-bounce attenuation, >= 1; see
+ * vcrt_oracle.c). INT32_MIN when no scale holds the scene (oracle_render then returns -1). */
+int32_t oracle_scale_log2(const oracle_sphere* world, int32_t n, int32_t max_depth,
+                          int32_t quantum);
+
 /* Per-pixel radiance of one sample (ray_color), for KATs. */
 void oracle_ray_color(const oracle_sphere* world, int32_t n, const float origin[3],
                       const float dir[3], int32_t max_depth, float out[3], uint64_t* segments);

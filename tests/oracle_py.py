@@ -73,6 +73,9 @@ class Oracle:
         L.oracle_scene_generator_text.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_reference_constants.restype = None
         L.oracle_reference_constants.argtypes = [ctypes.c_void_p]
+        L.oracle_scale_log2.restype = ctypes.c_int32
+        L.oracle_scale_log2.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_int32]
         L.oracle_scene_random_spheres.restype = ctypes.c_int32
         L.oracle_scene_random_spheres.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_void_p,
                                                                          ctypes.c_int32]
@@ -123,6 +126,12 @@ class Oracle:
         return dict(chunk=stats["accumulate_chunk"], tail=stats["accumulate_tail"],
                     tail_chunk=stats["accumulate_tail_chunk"],
                     quantum=stats["accumulate_quantum"])
+
+    def scale_log2(self, spheres, max_depth: int, quantum: int) -> int:
+        """s of the quantization scale 2^s of the quantum sums (oracle_scale_log2);
+        -2**31 when no scale holds the scene."""
+        spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+        return self.lib.oracle_scale_log2(spheres.ctypes.data, len(spheres), max_depth, quantum)
 
     # ---- render ----
     def render(self, cfg: OracleConfig, spheres: np.ndarray, rows=None, threads: int = 0):
@@ -202,7 +211,24 @@ class Oracle:
             self._s((0, -1000, 0), 1000.0, (0.5, 0.5, 0.5), 1, 1.0),
         ])
 
+    def bright_scene(self, param: float = 3.0) -> np.ndarray:
+        """A test scene (not the reference's) whose radiance passes 1 per sample: white
+        Lambertian ground and balls with param (the reference's unbounded "reflect ratio",
+        textures.glsl:22) > 1, so that a path's attenuation grows with every bounce. Three big
+        balls and 16 small ones (the culled scans need >= 16 spheres)."""
+        parts = [self._s((0, 1.2, 0), 1.0, (1.0, 1.0, 1.0), 1, param),
+                 self._s((-2.2, 1.0, 0), 1.0, (0.9, 0.8, 0.7), 1, param),
+                 self._s((2.2, 1.0, 0), 1.0, (0.8, 0.9, 1.0), 1, param)]
+        for k in range(16):
+            x, z = -3.0 + 0.4 * k, 1.6 + 0.3 * (k % 3)
+            parts.append(self._s((x, 0.15, z), 0.15, (1.0, 0.9 - 0.02 * k, 0.6 + 0.02 * k), 1,
+                                 param))
+        parts.append(self._s((0, -1000, 0), 1000.0, (1.0, 1.0, 1.0), 1, param))
+        return np.concatenate(parts)
+
     def scene(self, name: str) -> np.ndarray:
+        if name == "bright":
+            return self.bright_scene()
         if name == "final":
             return np.concatenate([self.random_spheres(-11, 11), self.big_three_and_ground()])
         if name == "three":

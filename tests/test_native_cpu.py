@@ -320,8 +320,8 @@ def test_work_chunk_rule(w, h, spp):
     """vcrt_work_chunk (the head's samples per work item; host only): the same for every rank of
     a sharded frame, at most spp, whole quanta, and an explicit accumulate_chunk rounded up to
     whole quanta. Checked against the rule restated here (64, halved while the largest rank has
-    < 2^24 - 2^21 items, down to 16, or to 32 for frames of fewer than 2^22 items at 32; at least
-    spp / 512; then whole quanta)."""
+    < 2^24 - 2^21 items or a pixel has fewer than 16 items, down to 16; at least spp / 512; then
+    whole quanta)."""
     q = _quantum_rule(spp)
     for world in (1, 2, 3, 8):
         ks = {vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
@@ -333,7 +333,8 @@ def test_work_chunk_rule(w, h, spp):
         assert k == spp or k % q == 0
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
         want = 64
-        while want > 16 and slots * -(-spp // want) < (1 << 24) - (1 << 21):
+        while want > 16 and (slots * -(-spp // want) < (1 << 24) - (1 << 21)
+                             or spp // want < 16):
             want //= 2
         assert k == min(_round_up(max(want, -(-spp // 512)), q), spp)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
@@ -342,6 +343,8 @@ def test_work_chunk_rule(w, h, spp):
         assert vc.renderer.work_chunk(vc.RenderDesc(
             width=w, height=h, samples_per_pixel=spp, world_size=world, accumulate_chunk=7,
             accumulate_quantum=1)) == min(7, spp)
+    if (w, h, spp) == (1920, 1080, 256):  # C3: K = 16 (16 items per pixel: the ring's reach)
+        assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp)) == 16
     if (w, h, spp) == (1920, 1080, 1024):  # the bench config: K = 64 / 64 / 32 / 16 on 1/2/4/8
         for world, want in ((1, 64), (2, 64), (4, 32), (8, 16)):
             assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
@@ -438,3 +441,84 @@ def test_work_chunk_rejects_invalid_desc():
     lib = N.lib()
     d = vc.RenderDesc(width=0, height=10, samples_per_pixel=4).to_c()
     assert lib.vcrt_work_chunk(ctypes.byref(d)) == N.VK_ERROR_INITIALIZATION_FAILED
+
+
+def _scaled_scene(oracle, param, albedo=1.0, material=1):
+    sc = oracle.scene("three").copy()
+    sc["texture"][:, 0] = material
+    sc["texture"][:, 1] = param
+    sc["colour"][:] = albedo
+    return sc
+
+
+@pytest.mark.parametrize("depth", [1, 8, 10, 50])
+@pytest.mark.parametrize("spp,quantum", [(64, 0), (1024, 0), (4096, 0), (64, 8), (100, 16)])
+def test_work_scale_rule_equals_oracle(oracle, depth, spp, quantum):
+    """vcrt_work_scale (the per-scene quantization scale 2^s of the quantum sums, host only)
+    equals the oracle's restatement of the rule (oracle_scale_log2) on the reference scenes (s =
+    32: the round-4 images are unchanged) and on scenes whose radiance passes 1 per sample
+    (Lambertian param > 1, textures.glsl:22; metal albedo > 1, :60): the largest s <= 32 with
+    G * A^depth * 2^s < 2^44."""
+    desc = vc.RenderDesc(width=64, height=36, samples_per_pixel=spp, max_depth=depth,
+                         accumulate_quantum=quantum)
+    g = vc.renderer.work_quantum(desc)
+    direct = g >= spp
+    scenes = [oracle.scene(n) for n in ("final", "three", "red", "stress4096", "bright")]
+    scenes += [_scaled_scene(oracle, p) for p in (0.5, 1.0, 1.5, 3.0, 10.0)]
+    scenes += [_scaled_scene(oracle, 1.0, albedo=2.5, material=2),  # a metal albedo > 1
+               _scaled_scene(oracle, 5.0, material=3)]             # glass keeps 1: param is eta
+    for sc in scenes:
+        want = 32 if direct else oracle.scale_log2(sc, depth, g)
+        if want < -80:  # no scale holds it: the product rejects the scene
+            with pytest.raises(N.VcrtError) as e:
+                vc.renderer.work_scale(desc, sc)
+            assert e.value.code == N.VK_ERROR_FORMAT_NOT_SUPPORTED
+            continue
+        assert vc.renderer.work_scale(desc, sc) == want
+        if not direct:  # G A^depth 2^s < 2^44 <= 2 G A^depth 2^s (unless s is capped at 32)
+            a = max([1.0] + [abs(float(c)) * abs(float(t[1])) if int(t[0]) == 1 else
+                             abs(float(c)) if int(t[0]) == 2 else 1.0
+                             for s in sc for c, t in ((c, s["texture"]) for c in s["colour"])])
+            r = g * a ** max(depth, 1)
+            assert r * 2.0 ** want < 2.0 ** 44
+            assert want == 32 or r * 2.0 ** (want + 1) >= 2.0 ** 44 * (1 - 1e-5)
+    for n in ("final", "three", "red", "stress4096"):  # the reference scenes keep s = 32
+        assert vc.renderer.work_scale(desc, n) == 32
+
+
+def test_work_scale_non_finite_and_out_of_range(oracle):
+    """Non-finite attenuations are left out of the bound (they only make radiance non-finite,
+    which makes the pixel NaN, as in the reference's sum); a bound no scale holds (R > 2^120)
+    is rejected with VK_ERROR_FORMAT_NOT_SUPPORTED by vcrt_work_scale and vcrt_set_scene, and the
+    oracle refuses to render it."""
+    desc = vc.RenderDesc(width=16, height=8, samples_per_pixel=64, max_depth=10)
+    sc = _scaled_scene(oracle, 1.0)
+    sc["texture"][0, 1] = np.nan
+    sc["colour"][1] = (np.inf, 0.5, 0.5)
+    assert vc.renderer.work_scale(desc, sc) == oracle.scale_log2(sc, 10, 4) == 32
+    huge = _scaled_scene(oracle, 1e4)  # (1e4)^10 = 2^133
+    with pytest.raises(N.VcrtError) as e:
+        vc.renderer.work_scale(desc, huge)
+    assert e.value.code == N.VK_ERROR_FORMAT_NOT_SUPPORTED
+    assert oracle.scale_log2(huge, 10, 4) == -2 ** 31
+    with pytest.raises(ValueError):
+        oracle.render(oracle.config(16, 8, 64, 10), huge)
+
+
+def test_bright_scene_needs_the_scale(oracle):
+    """The bright test scene (tests/oracle_py.py) passes the round-4 fixed scale's limit: at
+    depth 8 some quantum sums of 4 samples reach 2^12, where a fixed 2^32 scale turned pixels
+    NaN; with its own scale (s = 29) the oracle's image is finite and within 1e-6 relative RMS
+    of the reference's sequential fp32 sum."""
+    sc = oracle.scene("bright")
+    w, h, spp, depth = 160, 90, 16, 8
+    first, _ = oracle.render(oracle.config(w, h, 4, depth, quantum=4), sc)  # one quantum: S / 4
+    assert (first[..., :3] * 4).max() >= 4096.0
+    assert oracle.scale_log2(sc, depth, 4) == 29
+    img, _ = oracle.render(oracle.config(w, h, spp, depth, quantum=4), sc)
+    seq, _ = oracle.render(oracle.config(w, h, spp, depth, quantum=spp), sc)
+    assert np.isfinite(img).all()
+    d = img[..., :3].astype(np.float64) - seq[..., :3]
+    rel = np.sqrt((d ** 2).mean(axis=(0, 1))) / np.sqrt((seq[..., :3].astype(np.float64) ** 2)
+                                                        .mean(axis=(0, 1)))
+    assert (rel <= 1e-6).all(), rel

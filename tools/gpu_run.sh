@@ -16,6 +16,7 @@
 #   pmcab       instruction counters of one frame ($PMC_CFG, default c4) for the prev tree ($PREV),
 #               the current tree and the code objects in $OBJS: two PMC passes each, summarised by
 #               tools/pmc_ab_summary.py (VALU per wave-segment, issue, lane utilisation)
+#   trafficab   FETCH_SIZE / WRITE_SIZE (KB units) of one frame of $PMC_CFG, $PREV and current tree
 #   phases      stats build (VCRT_DEBUG_STATS=1): s_memtime per phase of the flat scan ($RO args)
 #   wavetimes   diagnostics build $WT_OBJ (VCRT_DEBUG_STATS=2): wave lifetimes ($WT_ARGS)
 set -o pipefail
@@ -77,18 +78,33 @@ mode_ab() {
   echo ab_done
 }
 
-mode_sweep() {
-  for i in $(seq 1 ${SWEEP_REPS:-1}); do
-    timeout -k 10 300 python tools/shard_sweep.py --spp 1024 --worlds ${WORLDS:-2,4,8} \
-      > $OUT/sweep_$i.json 2> $OUT/sweep_$i.err || { tail -20 $OUT/sweep_$i.err; return 1; }
-    python - "$OUT/sweep_$i.json" <<'PY'
+sweep_one() {  # tag, env prefix (or "none"), shard_sweep arguments...
+  local tag=$1 env=$2
+  shift 2
+  ( [ "$env" != none ] && export $env
+    timeout -k 10 300 python tools/shard_sweep.py --spp 1024 --worlds ${WORLDS:-2,4,8} "$@" \
+      > $OUT/sweep_$tag.json 2> $OUT/sweep_$tag.err ) || { tail -20 $OUT/sweep_$tag.err; return 1; }
+  python - "$OUT/sweep_$tag.json" "$tag" <<'PY'
 import json, sys
 r = json.load(open(sys.argv[1]))
 for key in sorted(x for x in r if x.startswith("world")):
     w = r[key]
-    print(f"full {r['full_ms']:.2f} ms {key}: max {w['max_ms']:.2f} sum {w['sum_ms']:.1f} "
-          f"estimate {w['ideal_efficiency']:.3f}")
+    print(f"{sys.argv[2]} full {r['full_ms']:.2f} ms {key}: max {w['max_ms']:.2f} "
+          f"sum {w['sum_ms']:.1f} estimate {w['ideal_efficiency']:.3f}")
 PY
+}
+
+mode_sweep() {  # $PREV: also the prev tree; $SWEEP_ENVS: env settings (A=1,B=2 ...); $SWEEP_OBJS
+  for i in $(seq 1 ${SWEEP_REPS:-1}); do
+    if [ -n "$PREV" ]; then sweep_one prev_$i VCRT_PKG_ROOT=$ROOT/$PREV || return 1; fi
+    sweep_one new_$i none || return 1
+    local j=0
+    for e in $SWEEP_ENVS; do
+      j=$((j+1)); sweep_one env${j}_$i "$(echo $e | tr , ' ')" || return 1
+    done
+    for o in $SWEEP_OBJS; do  # code objects of the current tree
+      sweep_one $(basename $o .hsaco)_$i none --code-object $ROOT/$o || return 1
+    done
   done
 }
 
@@ -141,6 +157,43 @@ mode_pmcab() {
     esac
   done
   python tools/pmc_ab_summary.py $P
+}
+
+mode_trafficab() {  # FETCH_SIZE / WRITE_SIZE of one frame ($PMC_CFG) for $PREV and the current tree
+  local P=$OUT/traffic RO=$(cfg_args ${PMC_CFG:-c3})
+  rm -rf $P && mkdir -p $P
+  for t in prev new; do
+    [ $t = prev ] && [ -z "$PREV" ] && continue
+    local env=VCRT_OBJ=none; [ $t = prev ] && env=VCRT_PKG_ROOT=$ROOT/$PREV
+    for c in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && export $env && timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv \
+        -d $P/${t}_$c -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${t}_$c.log 2>&1) \
+        || { tail -5 $P/${t}_$c.log; return 1; }
+    done
+  done
+  python - $P <<'PY'
+import collections, csv, os, sys
+P = sys.argv[1]
+for t in ("prev", "new"):
+    out = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        f = os.path.join(P, f"{t}_{c}", "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        agg, n = collections.defaultdict(float), collections.Counter()
+        for row in csv.DictReader(open(f)):
+            k = row["Kernel_Name"].split("(")[0]
+            if k.startswith("vcrt_trace") and row["Counter_Name"] == c:
+                agg[k] += float(row["Counter_Value"])
+                n[k] += 1
+        out[c] = {k: agg[k] / n[k] for k in agg}  # KB per dispatch
+    if out:
+        fe, wr = out.get("FETCH_SIZE", {}), out.get("WRITE_SIZE", {})
+        for k in sorted(set(fe) | set(wr)):
+            print(f"{t} {k}: FETCH_SIZE {fe.get(k, 0) / 1024:.1f} MB, WRITE_SIZE "
+                  f"{wr.get(k, 0) / 1024:.1f} MB, traffic (2 FETCH + WRITE) "
+                  f"{(2 * fe.get(k, 0) + wr.get(k, 0)) / 1024 ** 2:.3f} GB")
+PY
 }
 
 mode_phases() {

@@ -26,3 +26,10 @@ if len(d) > 31 and d[24]:
 if len(d) > 22 and d[22]:
     print("flat passes per wave-iter %.2f, partial %.2f; entries per live lane %.3f" % (
         d[22] / wi, d[21] / wi, d[19] / d[20]))
+if len(d) > 39 and d[33]:
+    print("loop top: retire %.1f%% of wave time (%.1f ticks per wave-iter), run in %.2f of "
+          "wave-iters, %.2f quanta per wave-iter" % (100 * d[32] / tot, d[32] / wi, d[38] / wi,
+                                                     d[39] / wi))
+    print("fetch loop in %.2f of wave-iters; blocks %.4f, items started %.3f, next items %.3f, "
+          "switches %.3f per wave-iter" % (d[33] / wi, d[34] / wi, d[35] / wi, d[36] / wi,
+                                           d[37] / wi))

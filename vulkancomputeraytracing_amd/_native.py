@@ -104,11 +104,12 @@ class vcrt_stats(ctypes.Structure):
         ("group_tests", ctypes.c_uint64),
         ("bound_tests", ctypes.c_uint64),
         ("kernel", ctypes.c_char * 48),
-        ("debug", ctypes.c_uint64 * 32),
+        ("debug", ctypes.c_uint64 * 64),
         ("accumulate_tail", ctypes.c_int32),
         ("accumulate_tail_chunk", ctypes.c_int32),
         ("ring_entries", ctypes.c_int32),
         ("accumulate_quantum", ctypes.c_int32),
+        ("accumulate_scale_log2", ctypes.c_int32),
     ]
 
 
@@ -124,6 +125,9 @@ SIGNATURES = {
     "vcrt_work_chunk": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_work_tail": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc),
                                         ctypes.POINTER(ctypes.c_int32)]),
+    "vcrt_work_scale": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc),
+                                         ctypes.POINTER(vcrt_sphere), ctypes.c_int32,
+                                         ctypes.POINTER(ctypes.c_int32)]),
     "vcrt_set_scene": (ctypes.c_int32, [ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_draw_next_frame": (ctypes.c_int32, []),
     "vcrt_end": (ctypes.c_int32, []),

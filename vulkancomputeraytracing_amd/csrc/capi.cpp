@@ -64,6 +64,7 @@ struct RendererState {
     bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
     bool stage_tables = true;    // VCRT_STAGE_TABLES=0: the SMEM scan reads its tables globally
     uint32_t ring_max = vcrt::kRingMaxEntries;
+    uint32_t nch_magic[2] = {0u, 0u};  // TraceParams.nch_magic of the partition
     uint32_t lds_per_cu = 0;     // LDS bytes per CU (160 KB on gfx950)
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     int debug_stats = 0;  // 1: the stats kernels; 2: the product kernels with a debug buffer
@@ -74,6 +75,7 @@ struct RendererState {
     int32_t nspheres = 0;
     bool scene_bounded = false;  // every |center|, radius <= 2^30: discriminants stay finite
     bool radii_safe = false;     // every |radius| in [2^-40, 2^30] (kFlagRadiiSafe)
+    int32_t accum_log2 = vcrt::kAccumMaxScaleLog2;  // the scene's accumulation scale s
     float4* d_geom = nullptr;  // pair-SoA groups of four (+1 padding group)
     float4* d_center_radius = nullptr;
     float4* d_shade = nullptr;
@@ -152,9 +154,18 @@ RendererState g;
 // decoupled and the claim-time ring clearing, C2 takes 0.878-0.894 ms at K = 16 against
 // 0.936-0.959 at K = 32 (K = 8: 0.882-0.896; profiles/r04_ab_log.md).
 constexpr uint64_t kChunkItems = (uint64_t{1} << 24) - (uint64_t{1} << 21);
+// Round 5: also halved (down to 16) while a pixel has fewer than kMinChunksPerPixel items: a
+// block (64 items, all chunks of 64 / nchunks pixels) then spans few pixels, so the wave's
+// 14-entry accumulation ring covers the pixels of its last ~3 blocks and long items keep their
+// entries (C3: K = 32 gave 9-pixel blocks, and most quanta missed the ring: 2.5 GB of atomics
+// per frame; VCRT_CHUNK_RULE=items restores the item-count rule alone).
+constexpr int32_t kMinChunksPerPixel = 16;
 int32_t default_chunk(uint64_t rank_slots, int32_t spp) {
+    const char* rule = std::getenv("VCRT_CHUNK_RULE");
+    const bool per_pixel = !(rule && std::strcmp(rule, "items") == 0);
     int32_t k = kDefaultChunk;
-    while (k > 16 && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems)
+    while (k > 16 && (rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems ||
+                      (per_pixel && spp / k < kMinChunksPerPixel)))
         k /= 2;
     const int32_t k_min = (spp + vcrt::kAccumMaxChunks - 1) / vcrt::kAccumMaxChunks;
     return std::max(k, k_min);
@@ -192,6 +203,40 @@ int32_t work_quantum(const vcrt_render_desc& d) {
     int32_t q = kDefaultQuantum;
     while ((d.samples_per_pixel + q - 1) / q > vcrt::kAccumMaxChunks) q *= 2;
     return q;
+}
+
+// The accumulation scale 2^s of a scene (vcrt_math.h "Accumulation"). One sample's radiance is
+// the sky's factor (<= 1) times the attenuations of its bounces: albedo * param for Lambertian
+// (textures.glsl:22), albedo for metal (:60), 1 for glass; so |radiance| <= R = A^depth, A the
+// largest per-bounce factor of the scene and at least 1 (the kernel's (int) of texture.x picks
+// the material; ids it cannot convert count as both). A quantum of G samples sums to at most
+// G R, and s is the largest integer <= 32 with G R 2^s < 2^44: every finite quantum sum then
+// quantizes below 2^44 and the pixel's exact sum stays below 2^53. The slack factors cover the
+// fp32 roundings (two per bounce, the sky's mix, the quantum's additions). Non-finite factors are
+// left out: they only make a sample's radiance non-finite, which makes its pixel NaN (its
+// quantum sum fails the 2^44 check). kAccumNoScale when R is beyond any scale (s < -80).
+constexpr int32_t kAccumNoScale = INT32_MIN;
+int32_t accum_scale_log2(const vcrt_sphere* sp, int32_t n, int32_t depth, int32_t quantum) {
+    double a = 1.0;
+    for (int32_t i = 0; i < n; i++) {
+        const float id = sp[i].texture[0];
+        const bool known = std::fabs(id) < 0x1p31f;  // (int) defined; NaN compares false
+        const int32_t t = known ? static_cast<int32_t>(id) : 0;
+        const bool lam = !known || t == VCRT_TEXTURE_LAMBERTIAN;
+        const bool met = !known || t == VCRT_TEXTURE_METAL;
+        for (int c = 0; c < 3; c++) {
+            const double col = std::fabs(static_cast<double>(sp[i].colour[c]));
+            const double f = col * std::fabs(static_cast<double>(sp[i].texture[1]));
+            if (lam && std::isfinite(f)) a = std::max(a, f);
+            if (met && std::isfinite(col)) a = std::max(a, col);
+        }
+    }
+    const double r = std::pow(a * (1.0 + 0x1p-22), std::max(depth, 1)) * (1.0 + 0x1p-20) *
+                     static_cast<double>(quantum) * (1.0 + static_cast<double>(quantum) * 0x1p-23);
+    if (!(r < 0x1p120)) return kAccumNoScale;
+    int32_t sc = vcrt::kAccumMaxScaleLog2;
+    while (sc > -80 && std::ldexp(r, sc) >= 0x1p44) --sc;
+    return std::ldexp(r, sc) < 0x1p44 ? sc : kAccumNoScale;
 }
 
 int32_t round_up(int32_t x, int32_t q) { return static_cast<int32_t>((int64_t{x} + q - 1) / q * q); }
@@ -245,6 +290,17 @@ int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk)
     kt = round_up(kt <= 0 ? std::max(4, chunk / 8) : kt, q);
     *tail_chunk = std::min(kt, t);
     return t;
+}
+
+// A multiplier m with (i * m) >> 32 == i / n for every item index i < 64 n of a part (the
+// chunk-minor slot split, TraceParams.nch_magic), checked here for every such i; 0 when there is
+// none (n <= 1, or n too large for the error term).
+uint32_t division_magic(uint32_t n) {
+    if (n <= 1u || n > 8192u) return 0u;
+    const uint64_t m = ((uint64_t{1} << 32) + n - 1u) / n;  // ceil(2^32 / n) < 2^32
+    for (uint64_t i = 0; i < 64ull * n; i++)
+        if (((i * m) >> 32) != i / n) return 0u;
+    return static_cast<uint32_t>(m);
 }
 
 // Jitter of sample indices base .. base+n-1 (shader.comp:48 depends only on the index).
@@ -347,29 +403,37 @@ hipError_t upload_near_far(const std::vector<float>& pairs, float4** out) {
     return hipMemcpy(*out, nf.data(), sizeof(float) * nf.size(), hipMemcpyHostToDevice);
 }
 
+// hipModuleGetFunction of a required entry point: a code object without it (e.g. an A/B build of
+// an older tree) is an incompatible shader binary, not an unknown error (hipErrorNotFound used to
+// map to VK_ERROR_UNKNOWN: profiles/r04_ab_log.md, run 7)
+#define VCRT_BIND(fn, m, name)                                                   \
+    do {                                                                         \
+        const hipError_t e_ = hipModuleGetFunction(fn, m, name);                 \
+        if (e_ == hipErrorNotFound) return VK_ERROR_INCOMPATIBLE_SHADER_BINARY_EXT; \
+        if (e_ != hipSuccess) return to_vk(e_);                                  \
+    } while (0)
+
 VkResult bind_kernels() {
     hipModule_t m = static_cast<hipModule_t>(g.stage.module);
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_lds, m, "vcrt_trace_lds"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem, m, "vcrt_trace_smem"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_assemble, m, "vcrt_assemble"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_fill, m, "vcrt_fill"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_resolve, m, "vcrt_resolve"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_encode, m, "vcrt_encode_srgb8"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_setup_jitter, m, "vcrt_setup_jitter"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_lds_stats, m, "vcrt_trace_lds_stats"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull, m, "vcrt_trace_cull"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_stats, m, "vcrt_trace_cull_stats"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds, m, "vcrt_trace_cull_lane_lds"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_stats, m,
-                                  "vcrt_trace_cull_lane_lds_stats"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane, m, "vcrt_trace_cull_lane"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_stats, m, "vcrt_trace_cull_lane_stats"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat, m, "vcrt_trace_cull_flat"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_stats, m, "vcrt_trace_cull_flat_stats"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_global, m, "vcrt_trace_cull_flat_global"));
-    VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_flat_global_stats, m,
-                                  "vcrt_trace_cull_flat_global_stats"));
+    VCRT_BIND(&g.k_trace_lds, m, "vcrt_trace_lds");
+    VCRT_BIND(&g.k_trace_smem, m, "vcrt_trace_smem");
+    VCRT_BIND(&g.k_assemble, m, "vcrt_assemble");
+    VCRT_BIND(&g.k_fill, m, "vcrt_fill");
+    VCRT_BIND(&g.k_resolve, m, "vcrt_resolve");
+    VCRT_BIND(&g.k_encode, m, "vcrt_encode_srgb8");
+    VCRT_BIND(&g.k_setup_jitter, m, "vcrt_setup_jitter");
+    VCRT_BIND(&g.k_trace_lds_stats, m, "vcrt_trace_lds_stats");
+    VCRT_BIND(&g.k_trace_smem_stats, m, "vcrt_trace_smem_stats");
+    VCRT_BIND(&g.k_trace_cull, m, "vcrt_trace_cull");
+    VCRT_BIND(&g.k_trace_cull_stats, m, "vcrt_trace_cull_stats");
+    VCRT_BIND(&g.k_trace_cull_lane_lds, m, "vcrt_trace_cull_lane_lds");
+    VCRT_BIND(&g.k_trace_cull_lane_lds_stats, m, "vcrt_trace_cull_lane_lds_stats");
+    VCRT_BIND(&g.k_trace_cull_lane, m, "vcrt_trace_cull_lane");
+    VCRT_BIND(&g.k_trace_cull_lane_stats, m, "vcrt_trace_cull_lane_stats");
+    VCRT_BIND(&g.k_trace_cull_flat, m, "vcrt_trace_cull_flat");
+    VCRT_BIND(&g.k_trace_cull_flat_stats, m, "vcrt_trace_cull_flat_stats");
+    VCRT_BIND(&g.k_trace_cull_flat_global, m, "vcrt_trace_cull_flat_global");
+    VCRT_BIND(&g.k_trace_cull_flat_global_stats, m, "vcrt_trace_cull_flat_global_stats");
     // optional: code objects built before the boxes-in-LDS flat scan lack it (A/B builds)
     if (hipModuleGetFunction(&g.k_trace_cull_flat_boxes, m, "vcrt_trace_cull_flat_boxes") !=
             hipSuccess ||
@@ -718,6 +782,21 @@ int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk) {
     return work_tail(*desc, work_chunk(*desc), tail_chunk);
 }
 
+vcrt_result vcrt_work_scale(const vcrt_render_desc* desc, const vcrt_sphere* spheres,
+                            int32_t count, int32_t* scale_log2) {
+    if (!desc || !desc_valid(*desc) || !scale_log2 || count < 0 || (count > 0 && !spheres))
+        return VCRT_ERROR_INITIALIZATION_FAILED;
+    const int32_t q = work_quantum(*desc);
+    if (q >= desc->samples_per_pixel && !desc->progressive) {  // one quantum per pixel
+        *scale_log2 = vcrt::kAccumMaxScaleLog2;
+        return VCRT_SUCCESS;
+    }
+    const int32_t sc = accum_scale_log2(spheres, count, desc->max_depth, q);
+    if (sc == kAccumNoScale) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
+    *scale_log2 = sc;
+    return VCRT_SUCCESS;
+}
+
 vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (!desc || !desc_valid(*desc)) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (g.begun) vcrt_end();
@@ -820,6 +899,8 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         g.tail_nchunks = t > 0 ? (t + g.tail_chunk - 1) / g.tail_chunk : 0;
     }
     g.nchunks = (g.tail_start + g.chunk - 1) / g.chunk;
+    g.nch_magic[0] = division_magic(static_cast<uint32_t>(g.nchunks));
+    g.nch_magic[1] = division_magic(static_cast<uint32_t>(g.tail_nchunks));
     if (g.nchunks >= 0x10000 || g.tail_nchunks >= 0x10000)  // the kernel's 16-bit chunk field
         return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
     // one quantum covers the pixel: the lane divides its fp32 sum (the reference's arithmetic)
@@ -883,6 +964,11 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
 vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (count < 0 || (count > 0 && !spheres)) return VCRT_ERROR_INITIALIZATION_FAILED;
+    // the quantization scale of the quantum sums for this scene (one quantum per pixel: none)
+    const int32_t scale_log2 =
+        g.direct ? vcrt::kAccumMaxScaleLog2
+                 : accum_scale_log2(spheres, count, g.desc.max_depth, g.quantum);
+    if (scale_log2 == kAccumNoScale) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
     // Scan table: groups of four spheres in pair-SoA form
     //   (cx0,cx1,cy0,cy1) (cz0,cz1,r0²,r1²) (cx2,cx3,cy2,cy3) (cz2,cz3,r2²,r3²),
     // r² = radius*radius as hit_sphere computes it (functions.glsl:18). The last group is
@@ -1006,6 +1092,8 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     g.stats.nspheres = count;
     g.accumulated = 0;  // a new scene restarts progressive accumulation
     if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
+    g.accum_log2 = scale_log2;
+    g.stats.accumulate_scale_log2 = scale_log2;
     g.scene_bounded = true;
     g.radii_safe = true;
     for (int32_t i = 0; i < count; i++) {
@@ -1096,6 +1184,9 @@ vcrt_result vcrt_draw_next_frame(void) {
                   (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
                   (g.direct ? vcrt::kFlagDirect : 0u);
         p.spp_total = static_cast<float>(spp_total);
+        p.accum_scale = std::ldexp(1.0f, g.accum_log2);
+        p.nch_magic[0] = g.nch_magic[0];
+        p.nch_magic[1] = g.nch_magic[1];
         for (int j = 0; j < 13; j++) p.sin_c[j] = vcrt::kSinC[j];
         const std::array<float, 12> cam = camera_array();
         for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
@@ -1168,7 +1259,7 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (!g.direct && !g.desc.progressive)  // every frame sums from zero
             VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
         if (g.debug_stats) {
-            unsigned long long init[32] = {0, 0, 0, 0, 0, ~0ull};
+            unsigned long long init[64] = {0, 0, 0, 0, 0, ~0ull};
             if (g.debug_stats == 2) init[9] = init[10] = ~0ull;  // wave times: minima
             VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
                                     g.stream));
@@ -1178,9 +1269,16 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
         if (!g.direct) {
-            vcrt::ResolveParams rp{g.d_accum,     g.d_fb,        static_cast<float>(spp_total),
-                                   g.desc.width,  g.desc.height, g.desc.rank,
-                                   g.desc.world_size, g.tiles_x, g.local_tiles};
+            vcrt::ResolveParams rp{g.d_accum,
+                                   g.d_fb,
+                                   std::ldexp(1.0, -g.accum_log2),
+                                   static_cast<float>(spp_total),
+                                   g.desc.width,
+                                   g.desc.height,
+                                   g.desc.rank,
+                                   g.desc.world_size,
+                                   g.tiles_x,
+                                   g.local_tiles};
             const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
             r = launch(g.k_resolve, rgrid, 256, 0, rp);
             if (r != VK_SUCCESS) return r;

@@ -9,13 +9,15 @@
 //   shaders/include/textures.glsl:19-71  lambertian / metal / glass scatter
 //
 // MI355X design:
-//   * Work items are (8x8 pixel tile, chunk of K samples, slot): one lane per pixel, the
-//     chunk's samples in order. A wave takes a whole block (one tile at one chunk = 64 items)
-//     with one atomic and hands its slots to lanes as they free up; a lane whose path ends
-//     starts its next sample at once (path regeneration). An item's fp32 sum, quantized to
-//     2^-32, is added exactly to the pixel's sums (three f64 atomics; vcrt_math.h
-//     "Accumulation") and vcrt_resolve divides: the image depends on the chunk size only, not
-//     on the schedule or the number of GPUs. One item per pixel: the lane writes the pixel.
+//   * Work items are (pixel, chunk of K samples): a block of 64 items holds all the chunks of a
+//     few pixels of one 8x8 tile (chunk-minor), and a wave takes a whole block with one atomic on
+//     its XCD's work queue and hands its items to lanes as they free up; a lane whose path ends
+//     starts its next sample at once (path regeneration). A lane sums its samples in fp32 in
+//     quanta of G (vcrt_math.h "Accumulation"); each quantum sum, quantized by the scene's scale
+//     2^s, is added exactly to the pixel's sums (LDS atomics into the wave's accumulation ring,
+//     flushed to global memory per pixel) and vcrt_resolve divides: the image depends on G and s
+//     only, not on the work items, the schedule or the number of GPUs. One quantum per pixel:
+//     the lane writes the pixel.
 //   * Ray state lives in VGPRs. Sphere tests run two spheres per packed-fp32 instruction
 //     (v_pk_add_f32 / v_pk_mul_f32 on pair-SoA groups of four: 2 lane-ops per issue, the only
 //     way gfx950 reaches its fp32 peak).
@@ -927,6 +929,10 @@ struct PhaseTicks {
     // lane sum, root-loop trips and lane sum; main shading hit lanes
     uint64_t cam_entries = 0, cam_lanes = 0, cam_live = 0, list_trips = 0, list_sum = 0,
              root_trips = 0, root_sum = 0, shade_hits = 0;
+    // the loop top: wave ticks in the retire, wave-iterations running the fetch loop, block
+    // fetches, items started, wave-iterations running the retire, quanta retired (lanes)
+    uint64_t retire = 0, fetch_iters = 0, blk_fetches = 0, items_cur = 0, retire_iters = 0,
+             quanta = 0;
 };
 
 __device__ __forceinline__ uint64_t ticks() { return __builtin_amdgcn_s_memtime(); }
@@ -1638,6 +1644,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             pargs = reinterpret_cast<const TraceParams*>(
                 (__attribute__((address_space(4))) const TraceParams*)(((uint64_t)hi << 32) | lo));
         }
+        uint64_t t_top = 0;
+        if constexpr (kStats) {
+            t_top = ticks();
+            const uint64_t fm = __ballot(fin);
+            pt.retire_iters += fm != 0u;
+            pt.quanta += (uint64_t)__popcll(fm);
+        }
         if (fin) {  // ---- retire the finished quantum: its sum to the pixel ----
             fin = false;
             if ((P.flags & kFlagDirect) != 0u) {
@@ -1647,20 +1660,21 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 P.out[out_index] = make_float4(acc.x / P.spp_total, acc.y / P.spp_total,
                                                acc.z / P.spp_total, 1.0f);
             } else {
-                // the chunk sum, quantized: RN_even(S * 2^32) (an integer below 2^44), summed
-                // exactly over the pixel's chunks in double; |S| >= 2^12, inf or NaN make the
-                // pixel NaN (vcrt_math.h "Accumulation")
-                // (three compares with |.| modifiers: NaN compares false; the NaN case in a real
-                // branch, so the common path converts without selects)
-                float ax = acc.x, ay = acc.y, az = acc.z;
-                if (!(fabsf(ax) < kAccumLimit && fabsf(ay) < kAccumLimit &&
-                      fabsf(az) < kAccumLimit)) {
+                // the quantum sum, quantized: RN_even(S * 2^s) (an integer below 2^44: the
+                // scene's scale, accum_scale), summed exactly over the pixel's quanta in double;
+                // |S * 2^s| >= 2^44 (infinite or NaN radiance) makes the pixel NaN (vcrt_math.h
+                // "Accumulation"). (Three compares with |.| modifiers: NaN compares false; the
+                // NaN case in a real branch, so the common path converts without selects.)
+                const float sc = P.accum_scale;
+                float ax = acc.x * sc, ay = acc.y * sc, az = acc.z * sc;
+                if (!(fabsf(ax) < kAccumQLimit && fabsf(ay) < kAccumQLimit &&
+                      fabsf(az) < kAccumQLimit)) {
                     asm volatile("");
                     ax = ay = az = __builtin_nanf("");
                 }
-                const double v0 = (double)__builtin_rintf(ax * kAccumScale);
-                const double v1 = (double)__builtin_rintf(ay * kAccumScale);
-                const double v2 = (double)__builtin_rintf(az * kAccumScale);
+                const double v0 = (double)__builtin_rintf(ax);
+                const double v1 = (double)__builtin_rintf(ay);
+                const double v2 = (double)__builtin_rintf(az);
                 const uint32_t qi = q & kQMask, ent = q >> kRingQBits;
                 // the pixel's ring entry while it still holds this pixel (LDS atomics; a claim
                 // that takes the entry for another pixel clears the lane's entry field), else
@@ -1691,12 +1705,16 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         // ---- lanes whose item is finished take the next slots of the wave's current block
         //      (one tile x chunk = 64 items); a new block costs one atomic per wave ----
         uint64_t t_fetch = 0;
-        if constexpr (kStats) t_fetch = ticks();
+        if constexpr (kStats) {
+            t_fetch = ticks();
+            pt.retire += t_fetch - t_top;
+        }
         // The loop only hands out slots; the lane state is set up once after it (setting it up
         // inside made the compiler copy ~20 live registers around the loop on every pass).
         bool got = false;
         uint32_t g_lt = 0u, g_chunk = 0u, g_slot = 0u, g_px = 0u, g_py = 0u, g_ent = 0u;
         uint64_t need_mask = __ballot(need && !done);
+        if constexpr (kStats) pt.fetch_iters += need_mask != 0u;
         while (need_mask) {
             if (blk_next >= 64u) {
                 if constexpr (kStats && kCull == 0) ++st_fetch;
@@ -1726,6 +1744,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     if (need) done = true;
                     break;
                 }
+                if constexpr (kStats) ++pt.blk_fetches;
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
                 blk_tail = b >= P.blocks_head;
@@ -1772,8 +1791,16 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             if (need && !done && mine < avail) {
                 uint32_t slot = blk_next + mine, ch = blk_chunk;
                 if (chunk_minor) {  // item 64 j + slot of the tile = (pixel, chunk), chunk-minor
+                    // i / n by the host's magic multiplier (exact for every i < 64 n, checked
+                    // by the host; 0: none): C4 8-way shards -1% against hipcc's division
+                    const uint32_t m = blk_tail ? P.nch_magic[1] : P.nch_magic[0];
                     const uint32_t i = 64u * blk_chunk + slot;
-                    slot = i / blk_nch;
+                    if (m != 0u) {
+                        slot = __umulhi(i, m);
+                    } else {
+                        asm volatile("");
+                        slot = i / blk_nch;
+                    }
                     ch = i - slot * blk_nch;
                 }
                 if (blk_tail) ch |= 0x10000u;  // chunk ch of the tail
@@ -1797,13 +1824,22 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             blk_next += min((uint32_t)__popcll(need_mask), avail);
             need_mask = __ballot(need && !done);
         }
+        if constexpr (kStats) pt.items_cur += (uint64_t)__popcll(__ballot(got));
         if (got) {
             q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
+            // the item's samples: the four partition values are wave-uniform, read by scalar
+            // loads and selected per lane (left to itself the compiler selected their kernarg
+            // addresses per lane and read them with vector loads, whose latency the jitter
+            // load's address then waited for: two dependent memory round trips per fetch)
             const bool tail = g_chunk >= 0x10000u;
-            const int k = tail ? P.tail_chunk : P.chunk;
-            sample = (tail ? P.tail_start : 0) + (int)(g_chunk & 0xffffu) * k;
-            sample_end = min(sample + k, tail ? P.spp : P.tail_start);
+            const int k_head = __builtin_amdgcn_readfirstlane(P.chunk);
+            const int k_tail = __builtin_amdgcn_readfirstlane(P.tail_chunk);
+            const int t_start = __builtin_amdgcn_readfirstlane(P.tail_start);
+            const int n_spp = __builtin_amdgcn_readfirstlane(P.spp);
+            const int k = tail ? k_tail : k_head;
+            sample = (tail ? t_start : 0) + (int)(g_chunk & 0xffffu) * k;
+            sample_end = min(sample + k, tail ? n_spp : t_start);
             // first camera ray of the chunk, shader.comp:48-52
             d = camera_dir(sample);
             o = cam;
@@ -2076,6 +2112,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             atomicAdd(P.debug + 29, (unsigned long long)pt.root_trips);
             atomicAdd(P.debug + 30, (unsigned long long)pt.root_sum);
             atomicAdd(P.debug + 31, (unsigned long long)pt.shade_hits);
+            atomicAdd(P.debug + 32, (unsigned long long)pt.retire);
+            atomicAdd(P.debug + 33, (unsigned long long)pt.fetch_iters);
+            atomicAdd(P.debug + 34, (unsigned long long)pt.blk_fetches);
+            atomicAdd(P.debug + 35, (unsigned long long)pt.items_cur);
+            atomicAdd(P.debug + 38, (unsigned long long)pt.retire_iters);
+            atomicAdd(P.debug + 39, (unsigned long long)pt.quanta);
         }
     }
 }
@@ -2205,15 +2247,16 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem_stats(TracePar
 // Exact sample sums -> pixels (vcrt_math.h "Accumulation"; shader.comp:56 divides by SPP).
 extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) {
     const uint32_t elems = p.local_tiles * 64u;
-    const double st = (double)p.spp_total;
+    const double st = (double)p.spp_total, inv = p.inv_scale;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < elems;
          q += gridDim.x * blockDim.x) {
         const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
                                   (uint32_t)p.world, (uint32_t)p.rank);
         if (!px.valid) continue;
         const double4 s = *reinterpret_cast<const double4*>(p.accum + 4u * q);
-        p.out[px.out_index] = make_float4(resolve_channel(s.x, st), resolve_channel(s.y, st),
-                                          resolve_channel(s.z, st), 1.0f);
+        p.out[px.out_index] = make_float4(resolve_channel(s.x, inv, st),
+                                          resolve_channel(s.y, inv, st),
+                                          resolve_channel(s.z, inv, st), 1.0f);
     }
 }
 

@@ -32,8 +32,8 @@ struct TraceParams {
     const float4* jitter;  // [spp] jx delta_u + jy delta_v, (jx, jy) = (-0.5+rand(i,i),
                            //   -0.5+rand(i+1,i+1)) of sample index i (shader.comp:48)
     float4* out;           // rank-local framebuffer, rgba32f (layout above)
-    double* accum;         // [local_tiles * 64][4] exact sums of the quantized chunk sums (r, g,
-                           //   b, unused), vcrt_math.h "Accumulation"; unused with kFlagDirect
+    double* accum;         // [local_tiles * 64][4] exact sums of the quantized quantum sums (r,
+                           //   g, b, unused), vcrt_math.h "Accumulation"; unused with kFlagDirect
     uint32_t* work;        // eight work-queue counters kQueueStride apart, zeroed every launch
     unsigned long long* segments;  // ray segments traced, zeroed before every launch
     unsigned long long* debug;     // diagnostics counters (stats kernels only), may be null
@@ -102,6 +102,11 @@ struct TraceParams {
     double sin_c[13];  // vcrt_math.h kSinC: the fast sine's constants, read by scalar loads
     const float4* corner;  // [local_tiles * 64] pixel00 + x delta_u + y delta_v per local slot
                            //   (shader.comp:43; vcrt_setup_jitter, the kernel's own operations)
+    // chunk-minor slots: (i * nch_magic[part]) >> 32 = i / nchunks of the head (0) / the tail (1)
+    // for every item index i < 64 nchunks (host-checked; 0: the kernel divides)
+    uint32_t nch_magic[2];
+    float accum_scale;  // 2^s, the quantization scale of the quantum sums (vcrt_math.h
+                        //   "Accumulation": per scene, accum_scale_log2)
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
@@ -148,6 +153,7 @@ struct SetupJitterParams {
 struct ResolveParams {
     const double* accum;              // [local_tiles * 64][4]
     float4* out;                      // rank-local framebuffer
+    double inv_scale;                 // 2^-s (TraceParams.accum_scale = 2^s)
     float spp_total;                  // samples per pixel accumulated so far (<= 2^19)
     int32_t width, height, rank, world;
     uint32_t tiles_x, local_tiles;

@@ -427,26 +427,29 @@ VCRT_HD float schlick_r0(float cosine, float r0) {
 
 // ---------------------------------------------------------------------------------------
 // Accumulation (shader.comp:46-56: color.rgb += ray_color(...); color /= SPP). The reference
-// sums a pixel's samples in fp32 in sample order. The GPU splits them into work items of K
-// samples (chunks, restarting at every progressive frame) and sums each chunk the same way.
-// One chunk per pixel (K >= spp, not progressive): color / SPP in fp32, the reference's
-// arithmetic exactly. Otherwise each chunk sum S is quantized to q = RN_even(S * 2^32) (the
-// scaling is exact; every fp32 S >= 2^-9 is kept exactly), the q are added in double -- exact,
-// as they are integers below 2^44 and a pixel has at most 512 chunks (< 2^53) -- and
-//     out = (float)((sum * 2^-32) / (double)spp_total).
-// Exact sums do not depend on the order of the additions, so the image is the same for any
-// schedule; it depends on K only (a sharded frame equals a one-GPU render with the same K).
-// The quantized combination differs from the fp32 sequential sum by less than that sum's own
-// rounding error. A chunk sum with
-// |S| >= 2^12, inf or NaN makes the pixel NaN (the reference scenes' radiance is <= 1 per
-// sample).
-constexpr float kAccumScale = 0x1p32f;
-constexpr float kAccumLimit = 4096.0f;
-constexpr int32_t kAccumMaxChunks = 512;  // chunks per pixel (progressive frames included)
+// sums a pixel's samples in fp32 in sample order. The GPU cuts them into quanta of G
+// consecutive samples (the accumulation quantum, restarting at every progressive frame; work
+// items hold whole quanta) and sums each quantum the same way. One quantum per pixel (G >= spp,
+// not progressive): color / SPP in fp32, the reference's arithmetic exactly. Otherwise each
+// quantum sum S is quantized to q = RN_even(S * 2^s) (the scaling is exact), the q are added in
+// double -- exact, as |q| < 2^44 and a pixel has at most 512 quanta (< 2^53) -- and
+//     out = (float)((sum * 2^-s) / (double)spp_total).
+// Exact sums do not depend on the order of the additions, so the image depends on G and s
+// alone: not on the work items, the schedule or the number of GPUs (a sharded frame equals the
+// one-GPU frame bit for bit). The scale 2^s is per scene (accum_scale_log2): the largest s <= 32
+// with G * R * 2^s < 2^44, R a bound on one sample's radiance (the largest per-bounce
+// attenuation of the scene, at least 1, raised to MAX_RECURSION_LEVEL), so every finite quantum
+// sum fits; the reference scenes (R ~ 1) take s = 32, which keeps every S >= 2^-9 exactly. The
+// quantized combination differs from the fp32 sequential sum by less than that sum's own
+// rounding error. A quantum sum with |S * 2^s| >= 2^44 -- only infinite or
+// NaN radiance reaches it -- makes the pixel NaN.
+constexpr int32_t kAccumMaxScaleLog2 = 32;
+constexpr float kAccumQLimit = 0x1p44f;   // |q| bound of one quantum sum
+constexpr int32_t kAccumMaxChunks = 512;  // quanta per pixel (progressive frames included)
 
-// One channel of a pixel from the exact sum of its quantized chunk sums.
-VCRT_HD float resolve_channel(double s, double spp_total) {
-    return (float)((s * 0x1p-32) / spp_total);
+// One channel of a pixel from the exact sum of its quantized quantum sums; inv_scale = 2^-s.
+VCRT_HD float resolve_channel(double s, double inv_scale, double spp_total) {
+    return (float)((s * inv_scale) / spp_total);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -88,6 +88,18 @@ def work_tail(desc: RenderDesc) -> tuple[int, int]:
     return (t, kt.value) if t > 0 else (0, 0)
 
 
+def work_scale(desc: RenderDesc, scene="final") -> int:
+    """s of the quantization scale 2^s of the quantum sums the renderer uses for `desc` and a
+    scene (vcrt_work_scale: host only, no GPU): the oracle restates the same rule."""
+    arr = builtin_scene(scene) if isinstance(scene, (str, int)) else scene
+    arr = np.ascontiguousarray(arr, dtype=SPHERE_DTYPE)
+    s = ctypes.c_int32(0)
+    N.check("vcrt_work_scale", N.lib().vcrt_work_scale(
+        ctypes.byref(desc.to_c()), arr.ctypes.data_as(ctypes.POINTER(N.vcrt_sphere)), len(arr),
+        ctypes.byref(s)))
+    return s.value
+
+
 def tiles_for_rank(width: int, height: int, world: int, rank: int) -> list[int]:
     """Row-major 8x8 tile indices (ty * tiles_x + tx) rank `rank` renders, in its local order:
     the tiles with (tx + ty) % world == rank (csrc/vcrt_math.h tile_of)."""
