@@ -796,6 +796,8 @@ def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth,
 
 @pytest.mark.parametrize("stage", ["1", "0"])
 @pytest.mark.parametrize("scene,w,h,spp,depth", [("three", 96, 54, 40, 8),   # staged: 1 KB
+                                                  ("red", 24, 16, 506, 3),   # 8192 B: staged
+                                                  ("red", 24, 16, 507, 3),   # 8208 B: global
                                                   ("red", 33, 21, 1200, 3),  # too big: global
                                                   ("final", 40, 24, 3, 10)])  # 485 spheres
 def test_smem_staged_tables_bitwise(oracle, monkeypatch, stage, scene, w, h, spp, depth):
@@ -809,7 +811,8 @@ def test_smem_staged_tables_bitwise(oracle, monkeypatch, stage, scene, w, h, spp
                                oracle.scene(scene))
     assert_bitwise(got, want, f"{scene} staged={stage}")
     assert st["segments"] == segs
-    staged = stage == "1" and 48 * st["nspheres"] + 8 * spp <= 8192
+    # the host's budget: 48 B of shading rows per sphere + a float4 jitter term per sample
+    staged = stage == "1" and 48 * st["nspheres"] + 16 * spp <= 8192
     assert (st["lds_bytes"] > 0) == staged
 
 

@@ -65,6 +65,8 @@ struct RendererState {
     bool stage_tables = true;    // VCRT_STAGE_TABLES=0: the SMEM scan reads its tables globally
     uint32_t ring_max = vcrt::kRingMaxEntries;
     uint32_t nch_magic[2] = {0u, 0u};  // TraceParams.nch_magic of the partition
+    // deferred fetches (TraceParams.fetch_min / fetch_wait; VCRT_FETCH_MIN, VCRT_FETCH_WAIT)
+    uint32_t fetch_min = 1u, fetch_wait = 0u;
     uint32_t lds_per_cu = 0;     // LDS bytes per CU (160 KB on gfx950)
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     int debug_stats = 0;  // 1: the stats kernels; 2: the product kernels with a debug buffer
@@ -101,7 +103,12 @@ struct RendererState {
     bool direct = false;  // one item per pixel, not progressive: lanes write pixels (kFlagDirect)
     double* d_accum = nullptr;  // [total_pixels][4] exact sums of the quantized chunk sums
     uint64_t accumulated = 0;               // samples per pixel accumulated (progressive)
-    std::vector<float2> jitter_host;
+    // the host's jitter (jx, jy) of a frame's sample indices: two pinned buffers used in turn,
+    // each reused only once the copy recorded by its event is done (progressive frames set up
+    // their jitter without waiting for the stream)
+    float2* h_jitter[2] = {nullptr, nullptr};
+    hipEvent_t ev_jitter[2] = {nullptr, nullptr};
+    int jitter_slot = 0;
     float* d_srgb_thresholds = nullptr;
     uchar4* d_srgb = nullptr;
     // per-frame inputs / outputs
@@ -304,8 +311,7 @@ uint32_t division_magic(uint32_t n) {
 }
 
 // Jitter of sample indices base .. base+n-1 (shader.comp:48 depends only on the index).
-void make_jitter(uint64_t base, int n, std::vector<float2>& out) {
-    out.resize(static_cast<size_t>(n));
+void make_jitter(uint64_t base, int n, float2* out) {
     for (int k = 0; k < n; k++) {
         const float i = static_cast<float>(base + k), i1 = static_cast<float>(base + k + 1);
         out[k].x = vcrt::kJitterOffset + vcrt::rand2(i, i);  // shader.comp:48
@@ -515,9 +521,13 @@ VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Pa
 // operations.
 VkResult setup_jitter(uint64_t base, bool corners = false) {
     const int spp = g.desc.samples_per_pixel;
-    make_jitter(base, spp, g.jitter_host);
-    VCRT_TRY(hipMemcpyAsync(g.d_jitter_in, g.jitter_host.data(), sizeof(float2) * spp,
+    const int slot = g.jitter_slot;
+    g.jitter_slot ^= 1;
+    VCRT_TRY(hipEventSynchronize(g.ev_jitter[slot]));  // its last copy (two frames ago) is done
+    make_jitter(base, spp, g.h_jitter[slot]);
+    VCRT_TRY(hipMemcpyAsync(g.d_jitter_in, g.h_jitter[slot], sizeof(float2) * spp,
                             hipMemcpyHostToDevice, g.stream));
+    VCRT_TRY(hipEventRecord(g.ev_jitter[slot], g.stream));
     vcrt::SetupJitterParams sp{};
     sp.jitter_in = g.d_jitter_in;
     sp.jitter = g.d_jitter;
@@ -531,10 +541,7 @@ VkResult setup_jitter(uint64_t base, bool corners = false) {
     sp.world = static_cast<uint32_t>(g.desc.world_size);
     const uint64_t total = static_cast<uint64_t>(spp) + (sp.corner ? sp.slots : 0u);
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((total + 255) / 256, 8192));
-    VkResult r = launch(g.k_setup_jitter, grid, 256, 0, sp);
-    if (r != VK_SUCCESS) return r;
-    VCRT_TRY(hipStreamSynchronize(g.stream));  // jitter_host is reused by the next frame
-    return VK_SUCCESS;
+    return launch(g.k_setup_jitter, grid, 256, 0, sp);
 }
 
 // State of the non-blocking communicator's last operations (comm_wait.hpp): done, still in
@@ -847,6 +854,13 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     // Jitter (shader.comp:48) depends only on the sample index: one table per frame config.
     const int spp = g.desc.samples_per_pixel;
     if ((r = to_vk(hipMalloc(&g.d_jitter_in, sizeof(float2) * spp))) != VK_SUCCESS) return fail(r);
+    for (int k = 0; k < 2; k++) {
+        if ((r = to_vk(hipHostMalloc(&g.h_jitter[k], sizeof(float2) * spp))) != VK_SUCCESS)
+            return fail(r);
+        if ((r = to_vk(hipEventCreateWithFlags(&g.ev_jitter[k], hipEventDisableTiming))) !=
+            VK_SUCCESS)
+            return fail(r);
+    }
     if ((r = to_vk(hipMalloc(&g.d_jitter, sizeof(float4) * spp))) != VK_SUCCESS) return fail(r);
     {
         float th[255];
@@ -937,6 +951,10 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (const char* e = std::getenv("VCRT_ITEM_ORDER"))
         if (std::strcmp(e, "tile") == 0) g.work_flags &= ~vcrt::kFlagChunkMinor;
     if (const char* e = std::getenv("VCRT_STAGE_TABLES")) g.stage_tables = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VCRT_FETCH_MIN"))
+        g.fetch_min = static_cast<uint32_t>(std::max(1, std::atoi(e)));
+    if (const char* e = std::getenv("VCRT_FETCH_WAIT"))
+        g.fetch_wait = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     if (const char* e = std::getenv("VCRT_ACCUM_RING")) {  // 0: off; n > 1: at most n entries
         // (clamped to kRingMaxEntries: a lane keeps its entry + 1 in the top bits of its pixel
         // index, so a larger ring would silently stop serving most pixels)
@@ -1182,9 +1200,12 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.blocks_head = g.local_tiles * static_cast<uint32_t>(g.nchunks);
         p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
                   (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
-                  (g.direct ? vcrt::kFlagDirect : 0u);
+                  (g.direct ? vcrt::kFlagDirect : 0u) |
+                  (static_cast<uint32_t>(g.accum_log2 + vcrt::kFlagScaleBias)
+                   << vcrt::kFlagScaleShift);
         p.spp_total = static_cast<float>(spp_total);
-        p.accum_scale = std::ldexp(1.0f, g.accum_log2);
+        p.fetch_min = g.fetch_min;
+        p.fetch_wait = g.fetch_wait;
         p.nch_magic[0] = g.nch_magic[0];
         p.nch_magic[1] = g.nch_magic[1];
         for (int j = 0; j < 13; j++) p.sin_c[j] = vcrt::kSinC[j];
@@ -1199,12 +1220,13 @@ vcrt_result vcrt_draw_next_frame(void) {
         p.stage_spheres = 0u;
         p.stage_spp = 0u;
         if (kc.f == g.k_trace_smem && g.nspheres > 0 && g.stage_tables) {
-            const uint32_t bytes = 48u * static_cast<uint32_t>(g.nspheres) +
-                                   16u * static_cast<uint32_t>(g.desc.samples_per_pixel);
+            // in 64 bits: 16 * spp wraps 32 bits for spp >= 2^28
+            const uint64_t bytes = 48ull * static_cast<uint64_t>(g.nspheres) +
+                                   16ull * static_cast<uint64_t>(g.desc.samples_per_pixel);
             if (bytes <= kStageMaxBytes) {
                 p.stage_spheres = static_cast<uint32_t>(g.nspheres);
                 p.stage_spp = static_cast<uint32_t>(g.desc.samples_per_pixel);
-                lds = (bytes + 15u) & ~15u;
+                lds = static_cast<uint32_t>((bytes + 15u) & ~15ull);
             }
         }
         const int variant = kc.variant;
@@ -1339,6 +1361,10 @@ vcrt_result vcrt_end(void) {
     free_scene();
     if (g.d_jitter) (void)hipFree(g.d_jitter);
     if (g.d_jitter_in) (void)hipFree(g.d_jitter_in);
+    for (int k = 0; k < 2; k++) {
+        if (g.h_jitter[k]) (void)hipHostFree(g.h_jitter[k]);
+        if (g.ev_jitter[k]) (void)hipEventDestroy(g.ev_jitter[k]);
+    }
     if (g.d_corner) (void)hipFree(g.d_corner);
     if (g.d_fb_own) (void)hipFree(g.d_fb_own);
     if (g.d_counters) (void)hipFree(g.d_counters);

@@ -1508,6 +1508,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     uint32_t blk_next = 64u, blk_lt = 0u, blk_chunk = 0u, blk_tx = 0u, blk_ty = 0u;
     uint32_t q_x = blockIdx.x & (kQueues - 1u), q_drained = 0u;  // the wave's queue; found empty
     uint32_t blk_nch = nchunks;  // chunks per pixel of the block's part (head or tail)
+    uint32_t fetch_waited = 0u;  // wave-iterations the fetch was deferred (flat scans)
     bool blk_tail = false;
     // the wave's accumulation ring (see RingEntry): next entry to hand out; the current block's
     // first pixel slot and first entry + 1 (0: the block's items add to global memory)
@@ -1661,11 +1662,13 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                                                acc.z / P.spp_total, 1.0f);
             } else {
                 // the quantum sum, quantized: RN_even(S * 2^s) (an integer below 2^44: the
-                // scene's scale, accum_scale), summed exactly over the pixel's quanta in double;
+                // scene's scale 2^s, from the flags word), summed exactly over the pixel's quanta in double;
                 // |S * 2^s| >= 2^44 (infinite or NaN radiance) makes the pixel NaN (vcrt_math.h
                 // "Accumulation"). (Three compares with |.| modifiers: NaN compares false; the
                 // NaN case in a real branch, so the common path converts without selects.)
-                const float sc = P.accum_scale;
+                // 2^s built from s + 128 in the flags' top byte (scalar ops, no load)
+                const float sc = __uint_as_float(
+                    ((P.flags >> kFlagScaleShift) + (127u - (uint32_t)kFlagScaleBias)) << 23);
                 float ax = acc.x * sc, ay = acc.y * sc, az = acc.z * sc;
                 if (!(fabsf(ax) < kAccumQLimit && fabsf(ay) < kAccumQLimit &&
                       fabsf(az) < kAccumQLimit)) {
@@ -1680,16 +1683,23 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // that takes the entry for another pixel clears the lane's entry field), else
                 // global memory (two branches: a pointer that may be either would make flat
                 // atomics, whose completion every later LDS wait would wait for)
+#ifdef VCRT_KO_RETIRE_ADD  // timing knock-out (wrong image): the quanta computed, not added
+                asm volatile("" ::"v"(v0), "v"(v1), "v"(v2), "v"(qi), "v"(ent));
+                if (false) {
+#else
                 if (ent != 0u) {
+#endif
                     double* s = ring[ent - 1u].s;
                     atomicAdd(s + 0, v0);
                     atomicAdd(s + 1, v1);
                     atomicAdd(s + 2, v2);
                 } else {
+#ifndef VCRT_KO_RETIRE_ADD
                     double* s = P.accum + 4u * qi;
                     atomicAdd(s + 0, v0);
                     atomicAdd(s + 1, v1);
                     atomicAdd(s + 2, v2);
+#endif
                 }
             }
             acc = mk(0.f, 0.f, 0.f);  // the next quantum (of this item or the next) sums from 0
@@ -1714,6 +1724,20 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         bool got = false;
         uint32_t g_lt = 0u, g_chunk = 0u, g_slot = 0u, g_px = 0u, g_py = 0u, g_ent = 0u;
         uint64_t need_mask = __ballot(need && !done);
+        if constexpr (kFlat) {
+            // deferred fetches (TraceParams.fetch_min / fetch_wait): while fewer than fetch_min
+            // lanes need an item and other lanes still have work, the wave skips the fetch for up
+            // to fetch_wait iterations (the waiting lanes idle; the fetch runs for more at once)
+            if (need_mask != 0u) {
+                if ((uint32_t)__popcll(need_mask) < P.fetch_min && fetch_waited < P.fetch_wait &&
+                    __ballot(!need && !done) != 0u) {
+                    ++fetch_waited;
+                    need_mask = 0u;
+                } else {
+                    fetch_waited = 0u;
+                }
+            }
+        }
         if constexpr (kStats) pt.fetch_iters += need_mask != 0u;
         while (need_mask) {
             if (blk_next >= 64u) {
@@ -1793,7 +1817,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 if (chunk_minor) {  // item 64 j + slot of the tile = (pixel, chunk), chunk-minor
                     // i / n by the host's magic multiplier (exact for every i < 64 n, checked
                     // by the host; 0: none): C4 8-way shards -1% against hipcc's division
+#ifdef VCRT_NO_MAGIC
+                    const uint32_t m = 0u;
+#else
                     const uint32_t m = blk_tail ? P.nch_magic[1] : P.nch_magic[0];
+#endif
                     const uint32_t i = 64u * blk_chunk + slot;
                     if (m != 0u) {
                         slot = __umulhi(i, m);
@@ -1833,10 +1861,15 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             // addresses per lane and read them with vector loads, whose latency the jitter
             // load's address then waited for: two dependent memory round trips per fetch)
             const bool tail = g_chunk >= 0x10000u;
+#ifdef VCRT_NO_SCALAR_PART
+            const int k_head = P.chunk, k_tail = P.tail_chunk, t_start = P.tail_start,
+                      n_spp = P.spp;
+#else
             const int k_head = __builtin_amdgcn_readfirstlane(P.chunk);
             const int k_tail = __builtin_amdgcn_readfirstlane(P.tail_chunk);
             const int t_start = __builtin_amdgcn_readfirstlane(P.tail_start);
             const int n_spp = __builtin_amdgcn_readfirstlane(P.spp);
+#endif
             const int k = tail ? k_tail : k_head;
             sample = (tail ? t_start : 0) + (int)(g_chunk & 0xffffu) * k;
             sample_end = min(sample + k, tail ? n_spp : t_start);

@@ -87,7 +87,9 @@ struct TraceParams {
     // to the pixel's sums at every sample index that is a multiple of G (vcrt_math.h
     // "Accumulation"); items hold whole quanta
     uint32_t quantum_mask;
-    uint32_t flags;        // kFlag*
+    uint32_t flags;        // kFlag*; bits 24..31: s + 128, the quantization scale 2^s of the
+                           //   quantum sums (vcrt_math.h "Accumulation": per scene), kept in
+                           //   the flags word the retire reads anyway (no load of its own)
     float spp_total;       // kFlagDirect: the divisor (samples per pixel)
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
     // Per-wave accumulation ring in LDS (tracer.hip "Accumulation ring"): ring_n entries of 32 B
@@ -105,8 +107,9 @@ struct TraceParams {
     // chunk-minor slots: (i * nch_magic[part]) >> 32 = i / nchunks of the head (0) / the tail (1)
     // for every item index i < 64 nchunks (host-checked; 0: the kernel divides)
     uint32_t nch_magic[2];
-    float accum_scale;  // 2^s, the quantization scale of the quantum sums (vcrt_math.h
-                        //   "Accumulation": per scene, accum_scale_log2)
+    // deferred fetches (the flat scans): a wave whose lanes still have work fetches items only
+    // once fetch_min lanes need one or it has deferred fetch_wait iterations (1, 0: every time)
+    uint32_t fetch_min, fetch_wait;
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
@@ -135,6 +138,8 @@ constexpr uint32_t kFlagChunkMinor = 8u;  // a block's 64 items run chunk-minor:
                                           // 64 / nchunks pixels (else one chunk of 64 pixels)
 constexpr uint32_t kFlagRadiiSafe = 16u;  // every |radius| in [2^-40, 2^30] (host-checked):
                                          // shading's (p - c) / r may take the unscaled division
+constexpr uint32_t kFlagScaleShift = 24u;  // TraceParams.flags: s + kFlagScaleBias
+constexpr int32_t kFlagScaleBias = 128;
 constexpr uint32_t kFlagDirect = 4u;  // one work item per pixel and frame, not progressive: the
                                       // lane writes the pixel itself (no sums, no resolve pass)
 
@@ -153,7 +158,7 @@ struct SetupJitterParams {
 struct ResolveParams {
     const double* accum;              // [local_tiles * 64][4]
     float4* out;                      // rank-local framebuffer
-    double inv_scale;                 // 2^-s (TraceParams.accum_scale = 2^s)
+    double inv_scale;                 // 2^-s (the scale of TraceParams.flags bits 24..31)
     float spp_total;                  // samples per pixel accumulated so far (<= 2^19)
     int32_t width, height, rank, world;
     uint32_t tiles_x, local_tiles;
