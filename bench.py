@@ -62,6 +62,12 @@ def parse():
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--min-warmup-seconds", type=float, default=0.3,
+                   help="after the W warmup steps, further untimed steps until the warmup has "
+                        "kept the GPU busy this long: the shader clock follows the load (a lone "
+                        "12-ms shard frame runs at ~2.15-2.30 GHz, sustained frames at ~2.38: "
+                        "profiles/r05_clock.txt), and the timed steps measure the steady state. "
+                        "Reported as warmup_extra; 0 turns it off")
     p.add_argument("--validate", action="store_true",
                    help="(the default) after the timed steps, rank 0 checks its frame: bit for "
                         "bit against the CPU oracle on pixels of a few full-width rows at full "
@@ -280,9 +286,26 @@ def main():
                 torch.cuda.current_stream().synchronize()
                 D.assemble_frame(r, gathered, frame, tiles_pad)
 
+    t_w = time.perf_counter()
     for i in range(args.warmup):
         step()
         log(f"[rank {rank}] warmup {i}: frame {r.stats()['frame_ms']:.1f} ms")
+    # extra warmup until the GPU has been busy for min_warmup_seconds (every rank runs the same
+    # count: rank 0 decides, so the collective draws stay matched)
+    extra = 0
+    if args.warmup > 0 and args.min_warmup_seconds > 0:
+        torch.cuda.synchronize()
+        frame_s = max(1e-4, (time.perf_counter() - t_w) / args.warmup)
+        extra = max(0, int((args.min_warmup_seconds - args.warmup * frame_s) / frame_s + 0.999))
+        extra = min(extra, 200)
+        if world > 1:
+            t = torch.tensor([extra], dtype=torch.int64)
+            dist.broadcast(t, src=0)
+            extra = int(t.item())
+        for i in range(extra):
+            step()
+        if extra:
+            log(f"[rank {rank}] {extra} more warmup steps ({args.min_warmup_seconds} s of load)")
 
     def barrier():
         if world > 1:
@@ -365,6 +388,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra": extra,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "strong",

@@ -146,7 +146,7 @@ typedef struct vcrt_stats {
     uint64_t group_tests;  /* groups of four spheres put through the exact test, per wave */
     uint64_t bound_tests;  /* group bounds tested, per wave (CULL variant) */
     char kernel[48];       /* the tracer kernel the last frame launched (its code-object symbol) */
-    uint64_t debug[64]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
+    uint64_t debug[128]; /* diagnostics (VCRT_DEBUG_STATS=1): [0..7] wave-iterations,
                            active-lane sum, hit groups, fetches, last/first wave end time, sum
                            end time, waves; [8..16] wave clock ticks (s_memtime) in the scan,
                            its uniform levels, node / group / candidate passes (CULL_FLAT),
@@ -159,7 +159,9 @@ typedef struct vcrt_stats {
                            [32..39] flat scans: wave ticks in the retire, wave-iterations
                            running the fetch loop, block fetches, items started, next items
                            handed out, item switches in the shading, wave-iterations running
-                           the retire, quanta retired (lanes); [40..63] region counters */
+                           the retire, quanta retired (lanes); [40..111] region counters:
+                           wave-level entries into the tracer's counted regions (tracer.hip
+                           reg::*, in order), summed over the waves */
     int32_t accumulate_tail;       /* tail samples per pixel in effect (0: none) */
     int32_t accumulate_tail_chunk; /* samples per tail item in effect */
     int32_t ring_entries;          /* LDS accumulation ring entries per wave (0: none; the chunk

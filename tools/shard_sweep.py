@@ -53,11 +53,13 @@ res = {"full_ms": full, "spp": a.spp, "chunk_arg": a.chunk, "variant": a.variant
        "full_partition": [st["accumulate_chunk"], st["accumulate_tail"],
                           st["accumulate_tail_chunk"]]}
 for world in [int(x) for x in a.worlds.split(",")]:
-    per = []
+    per, work = [], []
     for rank in range(world):
         ms, st = timed(vc.RenderDesc(rank=rank, world_size=world, **base))
         per.append(ms)
+        work.append([st["segments"], st["group_tests"], st["bound_tests"]])
     res[f"world{world}"] = {"per_rank_ms": [round(x, 2) for x in per], "max_ms": max(per),
+                            "per_rank_segments_groups_bounds": work,
                             "sum_ms": sum(per), "chunk": st["accumulate_chunk"],
                             "tail": [st["accumulate_tail"], st["accumulate_tail_chunk"]],
                             "ideal_efficiency": full / (world * max(per))}

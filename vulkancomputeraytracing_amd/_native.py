@@ -104,7 +104,7 @@ class vcrt_stats(ctypes.Structure):
         ("group_tests", ctypes.c_uint64),
         ("bound_tests", ctypes.c_uint64),
         ("kernel", ctypes.c_char * 48),
-        ("debug", ctypes.c_uint64 * 64),
+        ("debug", ctypes.c_uint64 * 128),
         ("accumulate_tail", ctypes.c_int32),
         ("accumulate_tail_chunk", ctypes.c_int32),
         ("ring_entries", ctypes.c_int32),

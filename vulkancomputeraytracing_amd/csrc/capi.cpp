@@ -39,6 +39,8 @@ constexpr size_t kCounterBytes = 256 + vcrt::kMaxQueues * 4 * vcrt::kQueueStride
 // LDS for the SMEM scan's staged tables (a few spheres' shading rows and the jitter table)
 constexpr uint32_t kStageMaxBytes = 8192;
 constexpr int32_t kDefaultChunk = 64;        // samples per work item (upper end)
+constexpr uint32_t kRegionCount = 72;       // tracer.hip kRegions: region counters per wave
+constexpr uint32_t kRegionDebugBase = 40;   // their sums in vcrt_stats.debug[40..111]
 
 struct RendererState {
     bool begun = false;
@@ -73,6 +75,8 @@ struct RendererState {
                           //    (builds with VCRT_WAVE_END_TIMES record wave start/end times)
     uint32_t work_flags = 0;
     void* d_debug = nullptr;
+    uint32_t* d_region = nullptr;  // stats kernels: [waves][kRegionCount] region entry counts
+    size_t region_words = 0;
     // scene
     int32_t nspheres = 0;
     bool scene_bounded = false;  // every |center|, radius <= 2^30: discriminants stay finite
@@ -1204,6 +1208,7 @@ vcrt_result vcrt_draw_next_frame(void) {
                   (static_cast<uint32_t>(g.accum_log2 + vcrt::kFlagScaleBias)
                    << vcrt::kFlagScaleShift);
         p.spp_total = static_cast<float>(spp_total);
+        p.region = nullptr;
         p.fetch_min = g.fetch_min;
         p.fetch_wait = g.fetch_wait;
         p.nch_magic[0] = g.nch_magic[0];
@@ -1278,10 +1283,22 @@ vcrt_result vcrt_draw_next_frame(void) {
         g.stats.ring_entries = static_cast<int32_t>(p.ring_n);
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
         VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
+        if (g.debug_stats == 1) {  // the stats kernels' region counters, one row per wave
+            const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
+            if (words > g.region_words) {
+                if (g.d_region) (void)hipFree(g.d_region);
+                g.d_region = nullptr;
+                g.region_words = 0;
+                VCRT_TRY(hipMalloc(&g.d_region, words * sizeof(uint32_t)));
+                g.region_words = words;
+            }
+            VCRT_TRY(hipMemsetAsync(g.d_region, 0, words * sizeof(uint32_t), g.stream));
+            p.region = g.d_region;
+        }
         if (!g.direct && !g.desc.progressive)  // every frame sums from zero
             VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
         if (g.debug_stats) {
-            unsigned long long init[64] = {0, 0, 0, 0, 0, ~0ull};
+            unsigned long long init[128] = {0, 0, 0, 0, 0, ~0ull};
             if (g.debug_stats == 2) init[9] = init[10] = ~0ull;  // wave times: minima
             VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
                                     g.stream));
@@ -1323,6 +1340,15 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (g.debug_stats)
             VCRT_TRY(hipMemcpy(g.stats.debug, g.d_debug, sizeof(g.stats.debug),
                                hipMemcpyDeviceToHost));
+        if (g.debug_stats == 1 && p.region) {  // region counters summed over the waves
+            const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
+            std::vector<uint32_t> rows(words);
+            VCRT_TRY(hipMemcpy(rows.data(), g.d_region, words * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost));
+            for (size_t w = 0; w < words / kRegionCount; w++)
+                for (uint32_t k = 0; k < kRegionCount; k++)
+                    g.stats.debug[kRegionDebugBase + k] += rows[w * kRegionCount + k];
+        }
         g.stats.grid_blocks = static_cast<int32_t>(grid);
         g.stats.block_threads = static_cast<int32_t>(block);
         g.stats.kernel_variant = variant;
@@ -1369,6 +1395,7 @@ vcrt_result vcrt_end(void) {
     if (g.d_fb_own) (void)hipFree(g.d_fb_own);
     if (g.d_counters) (void)hipFree(g.d_counters);
     if (g.d_debug) (void)hipFree(g.d_debug);
+    if (g.d_region) (void)hipFree(g.d_region);
     DestroyShaderStage(&g.stage);
     if (g.ev_start) (void)hipEventDestroy(g.ev_start);
     if (g.ev_stop) (void)hipEventDestroy(g.ev_stop);

@@ -66,6 +66,33 @@ __device__ __forceinline__ void tally_lds(uint32_t* slot, uint32_t x) {
     if ((threadIdx.x & 63u) == first) atomicAdd(slot, x);
 }
 
+// Region counters of the stats builds (tools/valu_attrib.py): one global atomic by the wave's
+// first active lane into the wave's own row of TraceParams.region ([waves][kRegions]) each time
+// the wave enters a counted region with some lane active. The product kernels pass a null row,
+// which folds every call away.
+namespace reg {
+enum : uint32_t {
+    kIter = 0, kRetire, kRetireNan, kRetireRing, kRetireGlobal, kNewRay, kFetchTrip, kBlock,
+    kBlockRing, kItem, kCam, kCamBig, kCamBigM0, kCamBigM1, kCamBigM2, kCamBigM3, kCamListTrip,
+    kCamRootTrip, kShadeCam, kScan, kScanLinear, kMainBig, kMainBigM0, kMainBigM1, kMainBigM2,
+    kMainBigM3, kListed, kLevelChunk, kLevelNodes, kDrainTrip, kPassCand, kPassGroup, kPassNode,
+    kPassChunk, kShadeSkyMain, kSqrtFallback, kDivFallback,
+    kShadeBase0 = 40, kShadeBase1 = 56,  // the shading's regions, per call site (camera phase,
+                                         // main-scan sky), at these offsets:
+    kShEntry = 0, kShHit, kShNormalDiv, kShSinFallback, kShLamMetal, kShLam, kShMetal, kShGlass,
+    kShGlassIn, kShGlassOut, kShGlassRefract, kShSky, kShEnded, kShNewRay, kShItemEnd,
+    kCount = 72
+};
+}  // namespace reg
+constexpr uint32_t kRegions = 72;  // the host's row size (vcrt_kernel_abi.h TraceParams.region)
+
+__device__ __forceinline__ void region(uint32_t* row, uint32_t k) {
+    if (row) {
+        const uint32_t first = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+        if ((threadIdx.x & 63u) == first) atomicAdd(row + k, 1u);
+    }
+}
+
 typedef __attribute__((address_space(4))) const float4 cfloat4;
 
 // A 32-bit constant materialized in a VGPR where it is used: the asm is volatile, so it is not
@@ -292,20 +319,23 @@ __device__ __forceinline__ float sqrt_unscaled(float x) {
 
 // Correctly rounded sqrt for any x: the unscaled sequence, and hipcc's full one in a real branch
 // for lanes outside [2^-96, inf] (tiny, zero, negative or NaN x).
-__device__ __forceinline__ float sqrt_fast(float x) {
+__device__ __forceinline__ float sqrt_fast(float x, uint32_t* rrow = nullptr) {
     float r = sqrt_unscaled(x);
     if (__ballot(!(x >= 0x1p-96f))) {  // wave-uniform: no exec-mask save and restore
         asm volatile("");
+        region(rrow, reg::kSqrtFallback);
         const float full = __builtin_sqrtf(x);
         r = !(x >= 0x1p-96f) ? full : r;
     }
     return r;
 }
 
-__device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a, float ya) {
+__device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a, float ya,
+                                                  uint32_t* rrow = nullptr) {
     float sq = sqrt_unscaled(disc);
     if (__ballot(disc < 0x1p-96f)) {  // wave-uniform: no exec-mask save and restore
         asm volatile("");  // a real branch: hipcc would otherwise run the full sqrt for every lane
+        region(rrow, reg::kSqrtFallback);
         const float full = __builtin_sqrtf(disc);
         sq = disc < 0x1p-96f ? full : sq;
     }
@@ -457,7 +487,8 @@ __device__ __forceinline__ uint32_t bound_pair_need(const BoxRay& r, const Bound
 // the big-sphere list, tested for every ray ahead of the hierarchy.
 __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay& r, v2f dx, v2f dy,
                                                     v2f dz, v2f a2, float a, float ya,
-                                                    float& max_t, int& best) {
+                                                    float& max_t, int& best,
+                                                    uint32_t* rrow = nullptr, uint32_t rb = 0) {
     const float4 q0 = rec[0], q1 = rec[1], idf = rec[4];
     v2f hb01, cc01, d01, hb23 = {0.f, 0.f}, cc23 = {0.f, 0.f}, d23 = {-1.f, -1.f};
     pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, q0, q1, hb01, cc01, d01);
@@ -466,14 +497,27 @@ __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay&
         pair_disc_cc(r.ox, r.oy, r.oz, dx, dy, dz, a2, rec[2], rec[3], hb23, cc23, d23);
     const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
     if (__ballot(!(m4 < 0.0f))) {
-        if (may_hit(hb01.x, cc01.x, d01.x))
-            consider(candidate_t_fast(hb01.x, d01.x, a, ya), __float_as_int(idf.x), max_t, best);
-        if (may_hit(hb01.y, cc01.y, d01.y))
-            consider(candidate_t_fast(hb01.y, d01.y, a, ya), __float_as_int(idf.y), max_t, best);
-        if (may_hit(hb23.x, cc23.x, d23.x))
-            consider(candidate_t_fast(hb23.x, d23.x, a, ya), __float_as_int(idf.z), max_t, best);
-        if (may_hit(hb23.y, cc23.y, d23.y))
-            consider(candidate_t_fast(hb23.y, d23.y, a, ya), __float_as_int(idf.w), max_t, best);
+        region(rrow, rb);
+        if (may_hit(hb01.x, cc01.x, d01.x)) {
+            region(rrow, rb + 1);
+            consider(candidate_t_fast(hb01.x, d01.x, a, ya, rrow), __float_as_int(idf.x), max_t,
+                     best);
+        }
+        if (may_hit(hb01.y, cc01.y, d01.y)) {
+            region(rrow, rb + 2);
+            consider(candidate_t_fast(hb01.y, d01.y, a, ya, rrow), __float_as_int(idf.y), max_t,
+                     best);
+        }
+        if (may_hit(hb23.x, cc23.x, d23.x)) {
+            region(rrow, rb + 3);
+            consider(candidate_t_fast(hb23.x, d23.x, a, ya, rrow), __float_as_int(idf.z), max_t,
+                     best);
+        }
+        if (may_hit(hb23.y, cc23.y, d23.y)) {
+            region(rrow, rb + 4);
+            consider(candidate_t_fast(hb23.y, d23.y, a, ya, rrow), __float_as_int(idf.w), max_t,
+                     best);
+        }
     }
 }
 
@@ -481,7 +525,9 @@ __device__ __forceinline__ void exact_group_uniform(cfloat4* rec, const CullRay&
 // member indices still come from the group record `rec`).
 __device__ __forceinline__ void exact_group_uniform_cam(cfloat4* crec, cfloat4* rec, v2f dx,
                                                         v2f dy, v2f dz, v2f a2, float a,
-                                                        float ya, float& max_t, int& best) {
+                                                        float ya, float& max_t, int& best,
+                                                        uint32_t* rrow = nullptr,
+                                                        uint32_t rb = 0) {
     const float4 c0 = crec[0], c1 = crec[1], idf = rec[4];
     v2f hb01, cc01, d01, hb23 = {0.f, 0.f}, cc23 = {0.f, 0.f}, d23 = {-1.f, -1.f};
     pair_disc_cam(dx, dy, dz, a2, c0, c1, hb01, cc01, d01);
@@ -489,14 +535,27 @@ __device__ __forceinline__ void exact_group_uniform_cam(cfloat4* crec, cfloat4* 
         pair_disc_cam(dx, dy, dz, a2, crec[2], crec[3], hb23, cc23, d23);
     const float m4 = fmaxf(fmaxf(d01.x, d01.y), fmaxf(d23.x, d23.y));
     if (__ballot(!(m4 < 0.0f))) {
-        if (may_hit(hb01.x, cc01.x, d01.x))
-            consider(candidate_t_fast(hb01.x, d01.x, a, ya), __float_as_int(idf.x), max_t, best);
-        if (may_hit(hb01.y, cc01.y, d01.y))
-            consider(candidate_t_fast(hb01.y, d01.y, a, ya), __float_as_int(idf.y), max_t, best);
-        if (may_hit(hb23.x, cc23.x, d23.x))
-            consider(candidate_t_fast(hb23.x, d23.x, a, ya), __float_as_int(idf.z), max_t, best);
-        if (may_hit(hb23.y, cc23.y, d23.y))
-            consider(candidate_t_fast(hb23.y, d23.y, a, ya), __float_as_int(idf.w), max_t, best);
+        region(rrow, rb);
+        if (may_hit(hb01.x, cc01.x, d01.x)) {
+            region(rrow, rb + 1);
+            consider(candidate_t_fast(hb01.x, d01.x, a, ya, rrow), __float_as_int(idf.x), max_t,
+                     best);
+        }
+        if (may_hit(hb01.y, cc01.y, d01.y)) {
+            region(rrow, rb + 2);
+            consider(candidate_t_fast(hb01.y, d01.y, a, ya, rrow), __float_as_int(idf.y), max_t,
+                     best);
+        }
+        if (may_hit(hb23.x, cc23.x, d23.x)) {
+            region(rrow, rb + 3);
+            consider(candidate_t_fast(hb23.x, d23.x, a, ya, rrow), __float_as_int(idf.z), max_t,
+                     best);
+        }
+        if (may_hit(hb23.y, cc23.y, d23.y)) {
+            region(rrow, rb + 4);
+            consider(candidate_t_fast(hb23.y, d23.y, a, ya, rrow), __float_as_int(idf.w), max_t,
+                     best);
+        }
     }
 }
 
@@ -947,10 +1006,11 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
                                            const float4* tbound, const float4* tnode, uint32_t ncg,
                                            const GroupTab<kGRec>& tg, const FlatRay& my,
                                            uint32_t& n_groups, uint32_t& n_bounds,
-                                           PhaseTicks& pt) {
+                                           PhaseTicks& pt, uint32_t* rrow = nullptr) {
     uint32_t nc = h.cand, ng = h.group, nn = h.node, nk = h.chunk;
     for (;;) {
         __builtin_amdgcn_wave_barrier();  // the entries were written by other lanes
+        region(rrow, reg::kDrainTrip);
         uint64_t t0 = 0;
         if constexpr (kStats) {
             t0 = ticks();
@@ -976,21 +1036,25 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         else if (nk >= nact) kind = 3;
         else if (th == 1u) kind = nk ? 3 : nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
+            region(rrow, reg::kPassCand);
             flat_pass<0, kFmt, kGRec, kNS>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
             }
         } else if (kind == 1) {
+            region(rrow, reg::kPassGroup);
             ++n_groups;
             flat_pass<1, kFmt, kGRec, kNS>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
+            region(rrow, reg::kPassNode);
             n_bounds += 8;
             flat_pass<2, kFmt, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else if (kind == 3) {
             if constexpr (WS::kHasChunks) {  // (nk stays 0 without the chunk stack)
+                region(rrow, reg::kPassChunk);
                 n_bounds += 8;
                 flat_pass<3, kFmt, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg,
                                                 tg, my);
@@ -1016,7 +1080,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                                                  const f3 o, const f3 d, bool primary,
                                                  uint32_t item, float& max_t, int& best,
                                                  uint32_t& groups_tested, uint32_t& bounds_tested,
-                                                 PhaseTicks& pt) {
+                                                 PhaseTicks& pt, uint32_t* rrow = nullptr) {
     uint64_t t_in = 0;
     if constexpr (kStats) t_in = ticks();
     // the camera-ray list record, loaded ahead of the big list so its latency overlaps it
@@ -1042,7 +1106,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
         const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {my.a, my.a};
         for (int gb = 0; gb < p.nbig; ++gb)  // the big spheres, for every ray (scalar loads)
             exact_group_uniform((cfloat4*)p.cgroup + 5 * gb, r, dx, dy, dz, a2, my.a, my.ya, max_t,
-                                best);
+                                best, rrow, reg::kMainBig);
     }
     if constexpr (kStats) pt.big += ticks() - t_in;
     uint32_t n_bounds = 0, n_groups = (uint32_t)p.nbig;
@@ -1058,6 +1122,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     const bool listed = (inf & 15u) != 15u;
     const uint32_t lcnt = listed ? inf & 15u : 0u, loff = inf >> 4;
     if (__ballot(lcnt != 0u)) {  // the stack height stays wave-uniform: prefix over all lanes
+        region(rrow, reg::kListed);
         uint32_t tot;
         uint32_t pos = wave_prefix<4>(lcnt, tot);
         h.group = tot;
@@ -1073,6 +1138,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     for (int base = 0;; base += 64) {
         uint32_t th = 1u;  // past the last chunk: drain everything
         if (base < ncg) {
+            region(rrow, reg::kLevelChunk);
             th = nact;
             uint64_t t0 = 0;
             if constexpr (kStats) t0 = ticks();
@@ -1085,6 +1151,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             const bool in_chunk = !listed && ((tops >> ((base >> 6) & 1)) & 1u) != 0;
             const uint64_t want = __ballot(in_chunk);
             if (want == 0) continue;
+            region(rrow, reg::kLevelNodes);
             if constexpr (kChunks) {
             // level 1 (many chunks): a chunk entry per lane whose ray may meet the chunk; chunk
             // passes test its nodes for that lane alone
@@ -1127,7 +1194,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             }
         }
         flat_drain<kStats, kFmt, kGRec, kNS>(th, nact, rank, lane, ws, h, tbound, tnode,
-                                         (uint32_t)ncg, tg, my, n_groups, n_bounds, pt);
+                                         (uint32_t)ncg, tg, my, n_groups, n_bounds, pt, rrow);
         if (base >= ncg) break;
     }
     __builtin_amdgcn_wave_barrier();
@@ -1455,6 +1522,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
              (threadIdx.x >> 6);
     }
     const uint32_t lane = threadIdx.x & 63u;
+    // stats builds: this wave's row of region counters (null in the product: calls fold away)
+    uint32_t* rrow = nullptr;
+    if constexpr (kStats) {
+        if (P.region)
+            rrow = P.region + (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kRegions;
+    }
     const f3 p00 = mk(P.cam[0], P.cam[1], P.cam[2]);
     const f3 du = mk(P.cam[3], P.cam[4], P.cam[5]);
     const f3 dv = mk(P.cam[6], P.cam[7], P.cam[8]);
@@ -1532,10 +1605,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
     // defer_ray: a sample that ends here leaves its next camera ray to the next iteration's fetch
     // (which sets up new items' first rays anyway; used after the main scan, whose lanes trace
     // that ray no earlier than the next camera fast trace)
-    auto shade_and_advance = [&](float max_t, int best, bool defer_ray) -> bool {
+    auto shade_and_advance = [&](float max_t, int best, bool defer_ray, uint32_t rb) -> bool {
         bool ended = false, fresh_cam = false;
         f3 contrib = mk(0.f, 0.f, 0.f);
+        region(rrow, rb + reg::kShEntry);
         if (best >= 0) {
+            region(rrow, rb + reg::kShHit);
             float4 cr, sh, mat;
             shading_rows<kStageable>(P, lds_dyn, best, cr, sh, mat);
             const f3 point = add(scale(max_t, d), o);
@@ -1549,6 +1624,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             const float nmax = fmaxf(fmaxf(fabsf(pcv.x), fabsf(pcv.y)), fabsf(pcv.z));
             if (!((P.flags & kFlagRadiiSafe) != 0u && nmin >= 0x1p-40f && nmax <= 0x1p30f)) {
                 asm volatile("");
+                region(rrow, rb + reg::kShNormalDiv);
                 normal = divs(pcv, cr.w);
             }
             const int type = (int)mat.x;
@@ -1557,33 +1633,43 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             // rand(dir.xy), rand(dir.xz), rand(dir.yz) for lambertian/metal (functions.glsl:43),
             // rand(point.xy) for glass (textures.glsl:51): three sines for every hit lane
             float s1, s2, s3;
+            bool sin_fb = false;
             sin3<true>((type == 3) ? rand_arg(point.x, point.y) : rand_arg(d.x, d.y),
                        rand_arg(d.x, d.z), rand_arg(d.y, d.z), s1, s2, s3,
-                       (cdouble*)&P.sin_c[0]);
+                       (cdouble*)&P.sin_c[0], kStats ? &sin_fb : nullptr);
+            if constexpr (kStats) {
+                if (__ballot(sin_fb)) region(rrow, rb + reg::kShSinFallback);
+            }
             const float r1 = rand_of_sin(s1);
             if (type == 1 || type == 2) {
+                region(rrow, rb + reg::kShLamMetal);
                 const float r2 = rand_of_sin(s2);
                 const float r3 = rand_of_sin(s3);
                 const f3 ru = mk(r1, r2, r3);  // random_in_unit_sphere(dir): normalize
-                const f3 u = divs(ru, sqrt_fast(dot(ru, ru)));
+                const f3 u = divs(ru, sqrt_fast(dot(ru, ru), rrow));
                 if (type == 1) {
+                    region(rrow, rb + reg::kShLam);
                     d = add(normal, u);
                     atten = scale(param, mul(atten, albedo));
                 } else {
+                    region(rrow, rb + reg::kShMetal);
                     d = add(reflect(d, normal), scale(param, u));
                     atten = mul(atten, albedo);
                 }
                 o = point;
             } else if (type == 3) {
+                region(rrow, rb + reg::kShGlass);
                 const f3 reflected = reflect(d, normal);
                 f3 outward;
                 float ni, cosine;
                 const float dn = dot(d, normal);
                 if (dn > 0.0f) {
+                    region(rrow, rb + reg::kShGlassIn);
                     outward = neg(normal);
                     ni = param;
-                    cosine = sqrt_fast(1.0f - param * param * (1.0f - dn * dn));
+                    cosine = sqrt_fast(1.0f - param * param * (1.0f - dn * dn), rrow);
                 } else {
+                    region(rrow, rb + reg::kShGlassOut);
                     outward = normal;
                     ni = mat.y;  // 1.0f / param
                     cosine = -dn;
@@ -1593,7 +1679,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 const float dt = dot(d, outward);
                 const float disc = 1.0f - ni * ni * (1.0f - dt * dt);
                 if (disc > 0.0f) {
-                    const float sd = sqrt_fast(disc);
+                    region(rrow, rb + reg::kShGlassRefract);
+                    const float sd = sqrt_fast(disc, rrow);
                     refracted = sub(scale(ni, sub(d, scale(dt, outward))), scale(sd, outward));
                     reflect_prob = schlick_r0(cosine, mat.z);  // schlick(cosine, param)
                 }
@@ -1603,15 +1690,18 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             ++pass;
             if (pass >= P.max_depth) ended = true;  // undefined GLSL return -> vec3(0)
         } else {
-            const float len = sqrt_fast(dot(d, d));  // length(d)
+            region(rrow, rb + reg::kShSky);
+            const float len = sqrt_fast(dot(d, d), rrow);  // length(d)
             contrib = mul(atten, sky_factor(d.y / len));
             ended = true;
         }
 
         if (ended) {
+            region(rrow, rb + reg::kShEnded);
             acc = add(acc, contrib);  // the quantum's fp32 sum in sample order
             ++sample;
             if (sample == sample_end) {
+                region(rrow, rb + reg::kShItemEnd);
                 // the item is done: its last quantum's sum in acc is retired at the top of the
                 // next iteration (few registers are live there: the accumulation code stays out
                 // of shading)
@@ -1624,6 +1714,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 if (defer_ray) {
                     newray = true;
                 } else {
+                    region(rrow, rb + reg::kShNewRay);
                     d = camera_dir(sample);
                     o = cam;
                     atten = mk(1.f, 1.f, 1.f);
@@ -1645,6 +1736,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             pargs = reinterpret_cast<const TraceParams*>(
                 (__attribute__((address_space(4))) const TraceParams*)(((uint64_t)hi << 32) | lo));
         }
+        region(rrow, reg::kIter);
         uint64_t t_top = 0;
         if constexpr (kStats) {
             t_top = ticks();
@@ -1653,6 +1745,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             pt.quanta += (uint64_t)__popcll(fm);
         }
         if (fin) {  // ---- retire the finished quantum: its sum to the pixel ----
+            region(rrow, reg::kRetire);
             fin = false;
             if ((P.flags & kFlagDirect) != 0u) {
                 // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
@@ -1673,6 +1766,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 if (!(fabsf(ax) < kAccumQLimit && fabsf(ay) < kAccumQLimit &&
                       fabsf(az) < kAccumQLimit)) {
                     asm volatile("");
+                    region(rrow, reg::kRetireNan);
                     ax = ay = az = __builtin_nanf("");
                 }
                 const double v0 = (double)__builtin_rintf(ax);
@@ -1684,27 +1778,29 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // global memory (two branches: a pointer that may be either would make flat
                 // atomics, whose completion every later LDS wait would wait for)
 #ifdef VCRT_KO_RETIRE_ADD  // timing knock-out (wrong image): the quanta computed, not added
+                constexpr bool kAdd = false;
                 asm volatile("" ::"v"(v0), "v"(v1), "v"(v2), "v"(qi), "v"(ent));
-                if (false) {
 #else
-                if (ent != 0u) {
+                constexpr bool kAdd = true;
 #endif
+                if (kAdd && ent != 0u) {
+                    region(rrow, reg::kRetireRing);
                     double* s = ring[ent - 1u].s;
                     atomicAdd(s + 0, v0);
                     atomicAdd(s + 1, v1);
                     atomicAdd(s + 2, v2);
-                } else {
-#ifndef VCRT_KO_RETIRE_ADD
+                } else if (kAdd) {
+                    region(rrow, reg::kRetireGlobal);
                     double* s = P.accum + 4u * qi;
                     atomicAdd(s + 0, v0);
                     atomicAdd(s + 1, v1);
                     atomicAdd(s + 2, v2);
-#endif
                 }
             }
             acc = mk(0.f, 0.f, 0.f);  // the next quantum (of this item or the next) sums from 0
         }
         if (newray) {  // the next sample's camera ray (shader.comp:48-52), deferred by the sky
+            region(rrow, reg::kNewRay);
             newray = false;
             d = camera_dir(sample);
             o = cam;
@@ -1740,6 +1836,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         }
         if constexpr (kStats) pt.fetch_iters += need_mask != 0u;
         while (need_mask) {
+            region(rrow, reg::kFetchTrip);
             if (blk_next >= 64u) {
                 if constexpr (kStats && kCull == 0) ++st_fetch;
                 // kQueues queues, each on workgroups of one XCD (workgroups are dispatched to
@@ -1769,6 +1866,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     break;
                 }
                 if constexpr (kStats) ++pt.blk_fetches;
+                region(rrow, reg::kBlock);
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
                 blk_tail = b >= P.blocks_head;
@@ -1787,6 +1885,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     const uint32_t ps0 = (64u * blk_chunk) / blk_nch;
                     const uint32_t np = (64u * blk_chunk + 63u) / blk_nch - ps0 + 1u;
                     if (np <= P.ring_n) {
+                        region(rrow, reg::kBlockRing);
                         if (lane < np)
                             ring_claim(ring, ring_pos + lane, P.ring_n, P.accum, ps0 + lane,
                                        blk_lt, (blk_ty << 16) | blk_tx, (uint32_t)P.width,
@@ -1854,6 +1953,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         }
         if constexpr (kStats) pt.items_cur += (uint64_t)__popcll(__ballot(got));
         if (got) {
+            region(rrow, reg::kItem);
             q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
             // the item's samples: the four partition values are wave-uniform, read by scalar
@@ -1910,6 +2010,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             float mt = __uint_as_float(vconst<0x47c35000u>());  // kInfinity
             int bst = (int)vconst<0xffffffffu>();                // -1
             if (__ballot(cam_now)) {
+                region(rrow, reg::kCam);
                 if constexpr (kStats) {
                     ++pt.cam_entries;
                     pt.cam_lanes += (uint64_t)__popcll(__ballot(cam_now));
@@ -1918,6 +2019,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 uint32_t iters = 0, roots = 0;
                 if (cam_now) {
                     ++segs;
+                    #ifdef VCRT_COST_MAP  // diagnostics: segments per pixel in the sums' unused fourth channel
+                    atomicAdd(P.accum + 4u * (q & kQMask) + 3u, 1.0);
+                    #endif
                     // A camera ray starts at the camera centre: its spheres' oc and cc come from
                     // camera-relative records (pair_disc_cam: same bits, half the arithmetic of
                     // pair_disc_cc); the roots take candidate_t_fast.
@@ -1926,13 +2030,14 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     const v2f dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z}, a2 = {aa, aa};
                     for (int gb = 0; gb < P.nbig; ++gb)  // the big spheres (scalar loads)
                         exact_group_uniform_cam(crec + 4 * gb, (cfloat4*)P.cgroup + 5 * gb, dx, dy,
-                                                dz, a2, aa, ya, mt, bst);
+                                                dz, a2, aa, ya, mt, bst, rrow, reg::kCamBig);
                     // the quarter's listed spheres, two per record (primary.cpp): the exact
                     // test's may-hit bits are collected first (bit 2k + s)...
                     const uint32_t cnt = inf & 15u;
                     const float4* lr = P.cam_rec + 4u * (uint32_t)P.nbig + 3u * (inf >> 4);
                     uint32_t cbits = 0u;
                     for (uint32_t k = 0; 2u * k < cnt; ++k) {
+                        region(rrow, reg::kCamListTrip);
                         ++iters;
                         const float4 q0 = lr[3u * k], q1 = lr[3u * k + 1u];
                         v2f hb, cc, dc;
@@ -1946,6 +2051,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     // sphere's hb and disc recomputed by the same operations (measured: both
                     // members' roots packed in the first loop issue more VALU, +1.8%)
                     while (cbits) {
+                        region(rrow, reg::kCamRootTrip);
                         const uint32_t b = (uint32_t)__builtin_ctz(cbits);
                         cbits &= cbits - 1u;
                         const float4* c = lr + 3u * (b >> 1);
@@ -1955,7 +2061,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                         const float ocz = hi ? zc.y : zc.x, cc = hi ? zc.w : zc.z;
                         const float hb = ocx * d.x + ocy * d.y + ocz * d.z;
                         const float disc = hb * hb - aa * cc;
-                        consider(candidate_t_fast(hb, disc, aa, ya),
+                        consider(candidate_t_fast(hb, disc, aa, ya, rrow),
                                  __float_as_int(hi ? id.y : id.x), mt, bst);
                         ++roots;
                     }
@@ -1988,7 +2094,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             }
             uint64_t t_cs = 0;
             if constexpr (kStats) t_cs = ticks();
-            if (cam_now || pending) fresh = shade_and_advance(mt, bst, false);
+            if (cam_now || pending) {
+                region(rrow, reg::kShadeCam);
+                fresh = shade_and_advance(mt, bst, false, reg::kShadeBase0);
+            }
             if constexpr (kStats) {
                 const uint64_t t1 = ticks();
                 pt.cam += t1 - t_cam;
@@ -1999,6 +2108,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 
         // ---- one segment: scan the whole sphere list (functions.glsl:73-81) ----
         ++segs;
+        #ifdef VCRT_COST_MAP  // diagnostics: segments per pixel in the sums' unused fourth channel
+        atomicAdd(P.accum + 4u * (q & kQMask) + 3u, 1.0);
+        #endif
         float max_t = __uint_as_float(vconst<0x47c35000u>());  // kInfinity
         int best = (int)vconst<0xffffffffu>();                   // -1
         uint32_t hit_groups = 0;
@@ -2009,6 +2121,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                                  aa <= 0x1p60f && fabsf(o.x) <= 0x1p30f &&
                                  fabsf(o.y) <= 0x1p30f && fabsf(o.z) <= 0x1p30f;
             if (__ballot(!guarded) == 0) {
+                region(rrow, reg::kScan);
                 uint32_t lane_cnt = 0;
                 uint64_t t0 = 0;
                 if constexpr (kStats) t0 = ticks();
@@ -2018,7 +2131,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 else if constexpr (kFlat)
                     scan_culled_flat<kStats, kFmt, kGRec, kChunks, kNS>(
                         P, tbound, tnode, tg, ws, o, d, pass == 0, q & kQMask, max_t, best, w_halves,
-                        w_bounds, pt);
+                        w_bounds, pt, rrow);
                 else
                     scan_culled_lane<kStats>(P, tbound, tgroup, o, d, max_t, best, w_halves,
                                              w_bounds, lane_cnt, hit_groups);
@@ -2029,6 +2142,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                     if constexpr (!kFlat) st_fetch += lane_cnt;
                 }
             } else {
+                region(rrow, reg::kScanLinear);
                 scan_spheres<false>(P, lds_geom, n, o, d, max_t, best, hit_groups);
                 if constexpr (kFlat)
                     tally_lds(&ws->work[0], 2u * (uint32_t)((n + 3) >> 2));
@@ -2056,10 +2170,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 pend_best = best >= 0 ? best : kPendSky;
                 fresh = false;  // the ray is traced (it may have been a camera ray)
             } else {
-                fresh = shade_and_advance(max_t, best, true);  // the sky
+                region(rrow, reg::kShadeSkyMain);
+                fresh = shade_and_advance(max_t, best, true, reg::kShadeBase1);  // the sky
             }
         } else {
-            fresh = shade_and_advance(max_t, best, false);
+            fresh = shade_and_advance(max_t, best, false, reg::kShadeBase0);
         }
         if constexpr (kStats) pt.shade += ticks() - t_shade;
 
@@ -2289,7 +2404,12 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) 
         const double4 s = *reinterpret_cast<const double4*>(p.accum + 4u * q);
         p.out[px.out_index] = make_float4(resolve_channel(s.x, inv, st),
                                           resolve_channel(s.y, inv, st),
-                                          resolve_channel(s.z, inv, st), 1.0f);
+                                          resolve_channel(s.z, inv, st),
+#ifdef VCRT_COST_MAP  // diagnostics: alpha = the pixel's segments (tracer VCRT_COST_MAP)
+                                          (float)s.w);
+#else
+                                          1.0f);
+#endif
     }
 }
 

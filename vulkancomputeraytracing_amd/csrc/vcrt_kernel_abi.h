@@ -110,6 +110,9 @@ struct TraceParams {
     // deferred fetches (the flat scans): a wave whose lanes still have work fetches items only
     // once fetch_min lanes need one or it has deferred fetch_wait iterations (1, 0: every time)
     uint32_t fetch_min, fetch_wait;
+    // stats builds only (VCRT_DEBUG_STATS=1): [waves][72] region entry counts (tracer.hip
+    // reg::*), zeroed before the launch; null otherwise
+    uint32_t* region;
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)

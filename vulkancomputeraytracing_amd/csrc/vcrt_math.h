@@ -350,7 +350,7 @@ __device__ __forceinline__ bool sin_fast_try_n(const float* xf, float* out,
 // canonically in one loop (one inlined copy of the fdlibm path instead of three).
 template <bool kTab = false>
 __device__ __forceinline__ void sin3(float a1, float a2, float a3, float& s1, float& s2,
-                                     float& s3, cdouble* kc = nullptr) {
+                                     float& s3, cdouble* kc = nullptr, bool* fell_back = nullptr) {
     const float a[2] = {a1, a2};
     float sv[2];
     bool ok = sin_fast_try_n<2, kTab>(a, sv, kc);
@@ -364,6 +364,7 @@ __device__ __forceinline__ void sin3(float a1, float a2, float a3, float& s1, fl
     }
     s1 = sv[0];
     s2 = sv[1];
+    if (fell_back) *fell_back = !ok;  // stats builds (tracer.hip region counters)
     if (!ok) {
 #pragma nounroll
         for (int j = 0; j < 3; ++j) {
