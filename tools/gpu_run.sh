@@ -202,6 +202,26 @@ mode_phases() {
   python tools/phases_report.py $OUT/phases.json
 }
 
+mode_valuattr() {  # region counts (stats build) and the product's SQ_INSTS_VALU, same frames ($RO)
+  local P=$OUT/valuattr RO=${RO:---spp 64 --frames 2}
+  rm -rf $P && mkdir -p $P
+  VCRT_DEBUG_STATS=1 timeout -k 10 200 python tools/render_once.py $RO > $P/stats.json || return 1
+  timeout -k 10 200 python tools/render_once.py $RO > $P/product.json || return 1
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES --output-format csv \
+     -d $P/pmc -o run -- python3 $ROOT/tools/render_once.py $RO > $P/pmc.log 2>&1) \
+    || { tail -20 $P/pmc.log; return 1; }
+  find $P/pmc -name '*counter_collection.csv' | head -1 | xargs -I{} cp {} $P/counters.csv
+  python - $P/counters.csv <<'PY'
+import csv, sys, collections
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "vcrt_trace" in r["Kernel_Name"]]
+per = collections.defaultdict(dict)
+for r in rows:
+    per[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
+for d in sorted(per):
+    print("dispatch", d, per[d])
+PY
+}
+
 mode_wavetimes() {
   VCRT_DEBUG_STATS=2 timeout -k 10 120 python tools/wave_times.py ${WT_OBJ:-ab_objs/wt.hsaco} \
     ${WT_ARGS:---spp 1024 --worlds 8} || return 1

@@ -1,7 +1,7 @@
 """Measured VALU attribution of the flat tracer kernel: the product code object's static VALU
 instructions per counted region (tracer.hip reg::*) times the number of times a wave executed
 that region in a stats-build frame of the same workload (VCRT_DEBUG_STATS=1: region counters in
-vcrt_stats.debug[40..111]), against the product's SQ_INSTS_VALU of the same frame.
+vcrt_stats.debug[40..127]), against the product's SQ_INSTS_VALU of the same frame.
 
 How an instruction gets its region: the -gline-tables-only build (identical instruction stream to
 the product, checked) symbolizes every instruction with its inline chain; walking the chain from
@@ -86,6 +86,8 @@ def main():
     p.add_argument("--sq-valu", type=float, required=True,
                    help="SQ_INSTS_VALU of the product frame (instructions, per dispatch)")
     p.add_argument("--json", default=None)
+    p.add_argument("--detail", action="append", default=[],
+                   help="region name: also list its static VALU per innermost source line")
     a = p.parse_args()
     if a.hsaco is None:
         a.hsaco = subprocess.run(["bash", os.path.join(ROOT, "tools", "mkab.sh"), "lt"],
@@ -98,12 +100,10 @@ def main():
                          if "if (fell_back) *fell_back = !ok;" in ln)
     lines = src.split("\n")
     ev = enum_values(src)
-    names = {}
-    for k, v in ev.items():  # the global regions, then the shading's offsets (kSh*)
-        if k.startswith("kSh") and k not in ("kShadeBase0", "kShadeBase1"):
-            continue
-        names.setdefault(v, k)
-    sh_names = {v: k for k, v in ev.items() if k.startswith("kSh") and not k.startswith("kShade")}
+    # the global regions, and the shading's offsets from its call site's base (kSh*)
+    is_sh = lambda k: k.startswith("kSh") and not k.startswith("kShade")  # noqa: E731
+    names = {v: k for k, v in ev.items() if not is_sh(k) and k != "kCount"}
+    sh_names = {v: k for k, v in ev.items() if is_sh(k)}
     marks = blocks(lines)
     insts = V.disasm(a.hsaco, a.kernel)
     prod = V.disasm(a.product, a.kernel)
@@ -176,9 +176,13 @@ def main():
         return -1  # prologue / epilogue: once per wave
 
     static = collections.Counter()
+    where = collections.defaultdict(collections.Counter)
     for ad, mn, _ in insts:
         if V.is_valu(mn):
-            static[region_of(chains[ad])] += 1
+            r = region_of(chains[ad])
+            static[r] += 1
+            f, fl, ln = chains[ad][0]
+            where[r][(fl, ln, f.split("(")[0][:40])] += 1
     st = json.load(open(a.stats))
     st = st[-1] if isinstance(st, list) else st
     d = st["debug"]
@@ -195,22 +199,30 @@ def main():
     def label(r):
         if r < 0:
             return "prologue/epilogue"
-        if r >= ev["kShadeBase1"]:
+        if r in names:
+            return names[r]
+        if ev["kShadeBase1"] <= r < ev["kShadeBase1"] + 16:
             return "shade(sky after scan)." + sh_names.get(r - ev["kShadeBase1"], "?")
-        if r >= ev["kShadeBase0"]:
+        if ev["kShadeBase0"] <= r < ev["kShadeBase0"] + 16:
             return "shade(camera phase)." + sh_names.get(r - ev["kShadeBase0"], "?")
-        return names.get(r, str(r))
+        return str(r)
     print(f"stats frame: {st['segments']} segments, {waves} waves, {d[0]} wave-iterations")
     print(f"{'dynamic VALU':>14} {'share':>6} {'static':>6} {'entries':>12}  region")
     for dyn, r, n, cnt in rows:
         name = label(r)
         print(f"{dyn:14.4g} {100 * dyn / total:5.1f}% {n:6d} {cnt:12d}  {name}")
+    for want in a.detail:
+        for r in static:
+            if label(r) == want:
+                print(f"-- {want}: static VALU by innermost source line")
+                for (fl, ln, f), n in sorted(where[r].items()):
+                    print(f"   {n:4d}  {fl}:{ln}  {f}")
     print(f"attributed total {total:.4g} VALU instructions; SQ_INSTS_VALU {a.sq_valu:.4g}: "
           f"ratio {total / a.sq_valu:.4f}")
     if a.json:
         json.dump({"kernel": a.kernel, "attributed": total, "sq_insts_valu": a.sq_valu,
                    "ratio": total / a.sq_valu,
-                   "regions": [{"region": ("prologue/epilogue" if r < 0 else names.get(r, str(r))),
+                   "regions": [{"region": label(r),
                                 "index": r, "static": n, "entries": cnt, "dynamic": dyn}
                                for dyn, r, n, cnt in rows]},
                   open(a.json, "w"), indent=1)

@@ -39,8 +39,8 @@ constexpr size_t kCounterBytes = 256 + vcrt::kMaxQueues * 4 * vcrt::kQueueStride
 // LDS for the SMEM scan's staged tables (a few spheres' shading rows and the jitter table)
 constexpr uint32_t kStageMaxBytes = 8192;
 constexpr int32_t kDefaultChunk = 64;        // samples per work item (upper end)
-constexpr uint32_t kRegionCount = 72;       // tracer.hip kRegions: region counters per wave
-constexpr uint32_t kRegionDebugBase = 40;   // their sums in vcrt_stats.debug[40..111]
+constexpr uint32_t kRegionCount = 88;       // tracer.hip kRegions: region counters per wave
+constexpr uint32_t kRegionDebugBase = 40;   // their sums in vcrt_stats.debug[40..127]
 
 struct RendererState {
     bool begun = false;

@@ -81,10 +81,12 @@ enum : uint32_t {
                                          // main-scan sky), at these offsets:
     kShEntry = 0, kShHit, kShNormalDiv, kShSinFallback, kShLamMetal, kShLam, kShMetal, kShGlass,
     kShGlassIn, kShGlassOut, kShGlassRefract, kShSky, kShEnded, kShNewRay, kShItemEnd,
-    kCount = 72
+    // sub-blocks of the flat scan's regions that run only on some of their entries
+    kPrefixSlow = 72, kLevelTop, kPushNode, kPushGroup, kPushLevel, kListedTrip,
+    kCount = 88
 };
 }  // namespace reg
-constexpr uint32_t kRegions = 72;  // the host's row size (vcrt_kernel_abi.h TraceParams.region)
+constexpr uint32_t kRegions = 88;  // the host's row size (vcrt_kernel_abi.h TraceParams.region)
 
 __device__ __forceinline__ void region(uint32_t* row, uint32_t k) {
     if (row) {
@@ -340,8 +342,15 @@ __device__ __forceinline__ float candidate_t_fast(float hb, float disc, float a,
         sq = disc < 0x1p-96f ? full : sq;
     }
     const float r1 = div_a(-hb - sq, a, ya);
-    if (r1 > kMinT) return r1;
-    return div_a(-hb + sq, a, ya);
+    // the far root only in waves where some lane rejects the near one (a wave-uniform branch:
+    // rays from outside the sphere take the near root; -1.5% VALU at C4, r05_valu_attrib.txt)
+    float t = r1;
+    if (__ballot(!(r1 > kMinT))) {
+        asm volatile("");
+        const float r2 = div_a(-hb + sq, a, ya);
+        t = r1 > kMinT ? r1 : r2;
+    }
+    return t;
 }
 
 // A member whose origin lies outside or on it (cc >= 0) while the ray points away from its
@@ -819,7 +828,8 @@ __device__ __forceinline__ unsigned long long pack_hit(float t, int idx) {
 // Otherwise (the drain at the end of the grid, where finished lanes are masked off and DPP
 // would read their stale registers): bit-sliced ballots, ~5 VALU per bit.
 template <int kBits>
-__device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
+__device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total,
+                                                uint32_t* rrow = nullptr) {
     if (__builtin_amdgcn_read_exec() == ~0ull) {
         int x = (int)c;
         x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -831,6 +841,7 @@ __device__ __forceinline__ uint32_t wave_prefix(uint32_t c, uint32_t& total) {
         total = (uint32_t)__builtin_amdgcn_readlane(x, 63);
         return (uint32_t)x - c;
     }
+    region(rrow, reg::kPrefixSlow);
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int b = 0; b < kBits; ++b) {
@@ -871,7 +882,8 @@ template <int kKind, int kFmt, bool kGRec, uint32_t kNS, class WS>
 __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_t nact,
                                           uint32_t rank, uint32_t lane, WS* ws,
                                           const float4* tbound, const float4* tnode, uint32_t ncg,
-                                          const GroupTab<kGRec>& tg, const FlatRay& my) {
+                                          const GroupTab<kGRec>& tg, const FlatRay& my,
+                                          uint32_t* rrow = nullptr) {
     using F = FlatFmt<kFmt>;
     using entry_t = typename F::entry_t;
     const uint32_t m = min(n, nact), top = n - m;
@@ -912,11 +924,12 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
             valid = (1u << min(8u, (ncg >> 3) - 8u * (e & F::kMask))) - 1u;
         uint32_t need = act ? (~gout & valid) : 0u;
         uint32_t tot;
-        uint32_t pos = pushed + wave_prefix<4>((uint32_t)__popc(need), tot);
+        uint32_t pos = pushed + wave_prefix<4>((uint32_t)__popc(need), tot, rrow);
         pushed += tot;
         if (need) {
             const uint32_t tag = (e & ~F::kMask) | ((e & F::kMask) << 3);
             do {
+                region(rrow, reg::kPushNode);
                 const uint32_t k = (uint32_t)__builtin_ctz(need);
                 need &= need - 1;
                 if constexpr (kKind == 2)
@@ -944,11 +957,12 @@ __device__ __forceinline__ void flat_pass(uint32_t& n, uint32_t& pushed, uint32_
         hits = push_sign(hits, hit_sign(hb01.x, cc01.x, d01.x));
         hits = act ? hits : 0u;
         uint32_t tot;
-        uint32_t pos = pushed + wave_prefix<3>((uint32_t)__popc(hits), tot);
+        uint32_t pos = pushed + wave_prefix<3>((uint32_t)__popc(hits), tot, rrow);
         pushed += tot;
         if (hits) {
             const uint32_t tag = e << 2;
             do {
+                region(rrow, reg::kPushGroup);
                 const uint32_t s = (uint32_t)__builtin_ctz(hits);
                 hits &= hits - 1;
                 ws->cand[pos++] = (typename F::cand_t)(tag | s);
@@ -1037,7 +1051,8 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         else if (th == 1u) kind = nk ? 3 : nn ? 2 : ng ? 1 : nc ? 0 : -1;
         if (kind == 0) {
             region(rrow, reg::kPassCand);
-            flat_pass<0, kFmt, kGRec, kNS>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<0, kFmt, kGRec, kNS>(nc, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my,
+                                           rrow);
             if constexpr (kStats) {
                 pt.cand += ticks() - t0;
                 ++pt.cand_passes;
@@ -1045,19 +1060,21 @@ __device__ __forceinline__ void flat_drain(uint32_t th, uint32_t nact, uint32_t 
         } else if (kind == 1) {
             region(rrow, reg::kPassGroup);
             ++n_groups;
-            flat_pass<1, kFmt, kGRec, kNS>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<1, kFmt, kGRec, kNS>(ng, nc, nact, rank, lane, ws, tbound, tnode, ncg, tg, my,
+                                           rrow);
             if constexpr (kStats) pt.group += ticks() - t0;
         } else if (kind == 2) {
             region(rrow, reg::kPassNode);
             n_bounds += 8;
-            flat_pass<2, kFmt, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my);
+            flat_pass<2, kFmt, kGRec, kNS>(nn, ng, nact, rank, lane, ws, tbound, tnode, ncg, tg, my,
+                                           rrow);
             if constexpr (kStats) pt.node += ticks() - t0;
         } else if (kind == 3) {
             if constexpr (WS::kHasChunks) {  // (nk stays 0 without the chunk stack)
                 region(rrow, reg::kPassChunk);
                 n_bounds += 8;
                 flat_pass<3, kFmt, kGRec, kNS>(nk, nn, nact, rank, lane, ws, tbound, tnode, ncg,
-                                                tg, my);
+                                                tg, my, rrow);
                 if constexpr (kStats) pt.levels += ticks() - t0;
             }
         } else {
@@ -1124,12 +1141,14 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
     if (__ballot(lcnt != 0u)) {  // the stack height stays wave-uniform: prefix over all lanes
         region(rrow, reg::kListed);
         uint32_t tot;
-        uint32_t pos = wave_prefix<4>(lcnt, tot);
+        uint32_t pos = wave_prefix<4>(lcnt, tot, rrow);
         h.group = tot;
         const uint16_t* ids = p.prim_ids + loff;
-        for (uint32_t k = 0; k < lcnt; ++k)
+        for (uint32_t k = 0; k < lcnt; ++k) {
+            region(rrow, reg::kListedTrip);
             ws->group[pos++] =
                 (typename FlatFmt<kFmt>::entry_t)((lane << FlatFmt<kFmt>::kShift) | ids[k]);
+        }
     }
     cfloat4* node = (cfloat4*)p.cnode;
     cfloat4* top = (cfloat4*)p.ctop;
@@ -1144,6 +1163,7 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
             if constexpr (kStats) t0 = ticks();
             // level 0, wave-uniform: the chunk's own bound (two chunks per test), per-lane bits
             if ((base & 127) == 0) {
+                region(rrow, reg::kLevelTop);
                 const BoundPair tp = load_bound_pair(top + 4 * (base >> 7));
                 tops = ~push_bound_pair(0u, br, tp.b0, tp.b1, tp.b2, tp.b3) & 3u;
                 n_bounds += 2;
@@ -1180,11 +1200,12 @@ __device__ __forceinline__ void scan_culled_flat(const TraceParams& p, const flo
                 t0 = t1;
             }
             uint32_t tot;
-            uint32_t pos = h.node + wave_prefix<4>((uint32_t)__popc(nodes), tot);
+            uint32_t pos = h.node + wave_prefix<4>((uint32_t)__popc(nodes), tot, rrow);
             h.node += tot;
             if (nodes) {
                 const uint32_t tag = (lane << FlatFmt<kFmt>::kShift) | ((uint32_t)base >> 3);
                 do {
+                    region(rrow, reg::kPushLevel);
                     const uint32_t j = (uint32_t)__builtin_ctz(nodes);
                     nodes &= nodes - 1;
                     ws->node[pos++] = (typename FlatFmt<kFmt>::entry_t)(tag | j);
