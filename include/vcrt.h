@@ -106,8 +106,8 @@ typedef struct vcrt_render_desc {
                                      progressive frame) in chunks of accumulate_tail_chunk, handed
                                      out after all the other work items, so that the items still
                                      running when the queue drains are short. 0 = the rule
-                                     (vcrt_work_tail), -1 = none. Part of the chunk partition: the
-                                     image depends on it as on accumulate_chunk. */
+                                     (vcrt_work_tail), -1 = none. Part of the chunk partition: it
+                                     schedules only; the image depends on the quantum alone. */
     int32_t accumulate_tail_chunk; /* samples per tail item; 0 = the rule. Tail and tail items
                                       are rounded to multiples of the quantum. */
     int32_t accumulate_quantum; /* the accumulation quantum G (a power of two; 0 = the rule,

@@ -356,8 +356,9 @@ def test_work_chunk_rule(w, h, spp):
 def test_work_tail_rule(w, h, spp):
     """vcrt_work_tail (the tail of the work partition; host only): the same for every rank,
     restated here -- T = 6 * K * 327680 / (64 * the largest rank's tiles) to the nearest power of
-    two, none when 4 T > spp or K >= spp, the head ending on a quantum boundary, items of one
-    quantum -- and explicit values (capped below spp, rounded to whole quanta) or -1 (none)."""
+    two, none when 4 T > spp or K >= spp or the head has >= 2 (2^24 - 2^21) items, the head ending
+    on a quantum boundary, items of max(4, K / 8) whole quanta -- and explicit values (capped
+    below spp, rounded to whole quanta) or -1 (none)."""
     import math
     q = _quantum_rule(spp)
     for world in (1, 2, 3, 8):
@@ -371,7 +372,8 @@ def test_work_tail_rule(w, h, spp):
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
         raw = 6 * 327680 * k / slots
         want = 0
-        if k < spp and raw >= 1:
+        many = slots * -(-spp // k) >= 2 * ((1 << 24) - (1 << 21))  # the head alone suffices
+        if k < spp and raw >= 1 and not many:
             want = 1 << round(math.log2(raw))
             if 4 * want > spp:
                 want = 0
@@ -391,7 +393,7 @@ def test_work_tail_rule(w, h, spp):
         d.accumulate_tail = -1
         assert vc.renderer.work_tail(d) == (0, 0)
     if (w, h, spp) == (1920, 1080, 1024):  # the bench config on 1/2/4/8 GPUs
-        for world, want in ((1, (64, 64, 8)), (2, (64, 128, 8)), (4, (32, 128, 4)),
+        for world, want in ((1, (64, 0, 0)), (2, (64, 128, 8)), (4, (32, 128, 4)),
                             (8, (16, 128, 4))):
             d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
             assert (vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d) == want

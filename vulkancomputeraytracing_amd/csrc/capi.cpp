@@ -287,6 +287,14 @@ int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk)
         uint32_t max_tiles = 0;
         for (int32_t rr = 0; rr < d.world_size; rr++)
             max_tiles = std::max(max_tiles, tiles_for_rank(d.width, d.height, d.world_size, rr));
+        // none when the head alone gives every lane many items (>= 2 kChunkItems: ~90 per lane):
+        // the drain is then a small part of the frame and the tail's short items cost more than
+        // they save. Measured round 5 (tools/ab.py, kernel ms, same bits): one GPU C4 89.68 ->
+        // 89.40 without the tail, C3 23.52 -> 23.14, C5 2518 -> 2497; with it, C4 2-way shards
+        // 45.18 against 46.07 and 4-way 23.21 against 23.33, 8-way 12.01 against 12.16.
+        const uint64_t head_items = 64ull * max_tiles *
+                                    static_cast<uint64_t>((spp + chunk - 1) / chunk);
+        if (head_items >= 2ull * kChunkItems) return 0;
         const double raw = static_cast<double>(kTailLaneItems) * chunk / (64.0 * max_tiles);
         if (raw < 1.0) return 0;
         t = 1 << static_cast<int>(std::lround(std::log2(raw)));  // nearest power of two
