@@ -4,7 +4,7 @@ per-rank fixed costs (launch, drain).
 
 Each renderer draws --frames frames back to back and reports the mean kernel time of the last
 half. The GPU's clock follows its load: a lone 12-ms shard frame after host work runs at ~2.29 GHz
-(GRBM_GUI_ACTIVE, profiles/r05_pmc_shards.txt) where the 90-ms full frame's second frame runs at
+(GRBM_GUI_ACTIVE, profiles/r05_clock.txt) where the 90-ms full frame's second frame runs at
 ~2.38 GHz, so the round-4 method (the second frame of each renderer) charged the shards ~3.5% of
 clock. On an 8-GPU node every GPU renders its shard frame after frame; the sustained frames are
 that steady state. --frames 2 --last 1 is the round-4 method."""
