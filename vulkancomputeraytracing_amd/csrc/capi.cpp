@@ -66,6 +66,7 @@ struct RendererState {
     bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
     bool stage_tables = true;    // VCRT_STAGE_TABLES=0: the SMEM scan reads its tables globally
     uint32_t ring_max = vcrt::kRingMaxEntries;
+    int max_blocks_per_cu = 0;  // VCRT_MAX_BLOCKS_PER_CU: caps the occupancy rule (0: none)
     uint32_t nch_magic[2] = {0u, 0u};  // TraceParams.nch_magic of the partition
     // deferred fetches (TraceParams.fetch_min / fetch_wait; VCRT_FETCH_MIN, VCRT_FETCH_WAIT)
     uint32_t fetch_min = 1u, fetch_wait = 0u;
@@ -967,6 +968,8 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         g.fetch_min = static_cast<uint32_t>(std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("VCRT_FETCH_WAIT"))
         g.fetch_wait = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+    if (const char* e = std::getenv("VCRT_MAX_BLOCKS_PER_CU"))  // cap on the occupancy rule
+        g.max_blocks_per_cu = std::max(1, std::atoi(e));
     if (const char* e = std::getenv("VCRT_ACCUM_RING")) {  // 0: off; n > 1: at most n entries
         // (clamped to kRingMaxEntries: a lane keeps its entry + 1 in the top bits of its pixel
         // index, so a larger ring would silently stop serving most pixels)
@@ -1254,6 +1257,7 @@ vcrt_result vcrt_draw_next_frame(void) {
                     hipSuccess ||
                 per_cu <= 0)
                 per_cu = 1;
+            if (g.max_blocks_per_cu > 0) per_cu = std::min(per_cu, g.max_blocks_per_cu);
         }
         // The accumulation ring (tracer.hip RingEntry): the LDS the workgroups leave free at
         // this occupancy, up to 63 entries of 32 B per wave, when the frame sums chunk sums
