@@ -169,6 +169,9 @@ typedef struct vcrt_stats {
     int32_t accumulate_quantum;    /* the accumulation quantum G in effect */
     int32_t accumulate_scale_log2; /* s of the quantization scale 2^s of the quantum sums (per
                                       scene: vcrt_work_scale) */
+    int32_t cost_order;            /* 1: the frame's blocks ran most expensive first (the order
+                                      measured by the configuration's first frame; frames with few
+                                      items per lane, or VCRT_WORK_ORDER=cost) */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera

@@ -794,6 +794,49 @@ def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth,
         assert st["ring_entries"] >= 8
 
 
+@pytest.mark.parametrize("scene,w,h,spp,depth,variant,tail,tail_chunk", [
+    ("three", 96, 54, 40, 8, vc.KERNEL_SMEM, 0, 0),
+    ("three", 37, 23, 48, 8, vc.KERNEL_SMEM, 16, 4),   # ragged edge tiles, a tail part
+    ("final", 40, 24, 12, 10, vc.KERNEL_LDS, 0, 0),
+])
+def test_cost_order_bitwise(oracle, monkeypatch, scene, w, h, spp, depth, variant, tail,
+                            tail_chunk):
+    """The cost-ordered schedule (VCRT_WORK_ORDER=cost; automatic for frames with few items per
+    lane): the first frame counts each pixel's segments (TraceParams.pixel_cost), the next hands
+    out the blocks most expensive first (block_order). Both frames are the oracle's image."""
+    monkeypatch.setenv("VCRT_WORK_ORDER", "cost")
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         kernel_variant=variant, accumulate_tail=tail,
+                         accumulate_tail_chunk=tail_chunk)
+    with vc.Renderer(desc, scene) as r:
+        r.draw_next_frame()
+        first, st1 = r.read_framebuffer(), r.stats()
+        r.draw_next_frame()
+        second, st2 = r.read_framebuffer(), r.stats()
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st1)),
+                               oracle.scene(scene))
+    assert (st1["cost_order"], st2["cost_order"]) == (0, 1)
+    assert_bitwise(first, want, f"{scene} measuring frame")
+    assert_bitwise(second, want, f"{scene} cost-ordered frame")
+    assert st1["segments"] == st2["segments"] == segs
+
+
+@pytest.mark.parametrize("scene,variant,cap", [("three", vc.KERNEL_SMEM, "3"),
+                                               ("final", vc.KERNEL_CULL_FLAT, "2")])
+def test_occupancy_cap_bitwise(oracle, monkeypatch, scene, variant, cap):
+    """VCRT_MAX_BLOCKS_PER_CU caps the occupancy rule's workgroups per CU (the grid shrinks to
+    cap x CUs) and keeps the LDS accumulation ring; the image is the oracle's."""
+    monkeypatch.setenv("VCRT_MAX_BLOCKS_PER_CU", cap)
+    w, h, spp, depth = 64, 36, 24, 8
+    got, st = gpu_render(scene, w, h, spp, depth, variant)
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
+                               oracle.scene(scene))
+    assert_bitwise(got, want, f"{scene} cap={cap}")
+    assert st["segments"] == segs
+    assert st["grid_blocks"] % int(cap) == 0 and st["grid_blocks"] <= 256 * int(cap)
+    assert st["ring_entries"] >= 8
+
+
 @pytest.mark.parametrize("stage", ["1", "0"])
 @pytest.mark.parametrize("scene,w,h,spp,depth", [("three", 96, 54, 40, 8),   # staged: 1 KB
                                                   ("red", 24, 16, 506, 3),   # 8192 B: staged

@@ -110,6 +110,7 @@ class vcrt_stats(ctypes.Structure):
         ("ring_entries", ctypes.c_int32),
         ("accumulate_quantum", ctypes.c_int32),
         ("accumulate_scale_log2", ctypes.c_int32),
+        ("cost_order", ctypes.c_int32),
     ]
 
 

@@ -67,6 +67,14 @@ struct RendererState {
     bool stage_tables = true;    // VCRT_STAGE_TABLES=0: the SMEM scan reads its tables globally
     uint32_t ring_max = vcrt::kRingMaxEntries;
     int max_blocks_per_cu = 0;  // VCRT_MAX_BLOCKS_PER_CU: caps the occupancy rule (0: none)
+    // the cost-ordered schedule ("cost order" in vcrt_draw_next_frame): -1 auto, 0 off, 1 on
+    // (VCRT_WORK_ORDER=cost / static); the first frame of a configuration measures each pixel's
+    // segments, later frames hand out the blocks most expensive first
+    int cost_order = -1;
+    uint32_t* d_pixel_cost = nullptr;   // [total_pixels] segments (TraceParams.pixel_cost)
+    uint32_t* d_block_order = nullptr;  // [blocks] TraceParams.block_order
+    size_t cost_words = 0, order_words = 0;
+    uint64_t order_key = 0;  // the configuration the order was measured for (0: none)
     uint32_t nch_magic[2] = {0u, 0u};  // TraceParams.nch_magic of the partition
     // deferred fetches (TraceParams.fetch_min / fetch_wait; VCRT_FETCH_MIN, VCRT_FETCH_WAIT)
     uint32_t fetch_min = 1u, fetch_wait = 0u;
@@ -957,6 +965,8 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     g.work_flags |= vcrt::kFlagReverseOrder;
     if (const char* e = std::getenv("VCRT_WORK_ORDER"))
         if (std::strcmp(e, "forward") == 0) g.work_flags &= ~vcrt::kFlagReverseOrder;
+    if (const char* e = std::getenv("VCRT_WORK_ORDER"))
+        g.cost_order = std::strcmp(e, "cost") == 0 ? 1 : 0;  // any other value: static order
     // A block's 64 items are all the chunks of 64 / nchunks pixels (chunk-minor): the camera
     // rays of a wave then come from a few pixels (+2.8% at the C4 workload against one chunk of
     // a whole tile, same bits). VCRT_ITEM_ORDER=tile restores the tile-wide blocks.
@@ -1124,6 +1134,7 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     g.nspheres = count;
     g.stats.nspheres = count;
     g.accumulated = 0;  // a new scene restarts progressive accumulation
+    g.order_key = 0;    // and its cost order is measured again
     if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
     g.accum_log2 = scale_log2;
     g.stats.accumulate_scale_log2 = scale_log2;
@@ -1138,6 +1149,63 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     }
     g.stage.pName = select_kernel().name;  // the entry point draws of this scene dispatch
     return VCRT_SUCCESS;
+}
+
+// Cost order (vcrt_draw_next_frame): at most this many items per lane of the persistent grid
+// make a frame drain-bound (C2: 3.7; C3, C4 on one GPU: ~100; C4 8-way shards: ~50).
+constexpr uint64_t kCostOrderItemsPerLane = 8;
+
+// The configuration a measured order belongs to: kernel, grid and partition (a new scene or
+// vcrt_begin resets it through order_key = 0).
+uint64_t order_key_of(hipFunction_t f, uint32_t grid, uint32_t total_blocks) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    mix(reinterpret_cast<uintptr_t>(f));
+    mix(grid);
+    mix(total_blocks);
+    mix(static_cast<uint64_t>(g.nchunks));
+    mix(static_cast<uint64_t>(g.tail_nchunks));
+    mix(g.local_tiles);
+    return h | 1u;
+}
+
+// From the pixels' segment counts of the frame just rendered: each part's blocks (head, then
+// tail) in decreasing cost, a block's cost being the segments of the pixels its 64 chunk-minor
+// items belong to (item i of tile lt's part with n chunks per pixel: slot i / n); ties in the
+// static order (bottom-up: the highest block first).
+VkResult build_block_order(uint32_t total_blocks) {
+    std::vector<uint32_t> cost(g.total_pixels);
+    VCRT_TRY(hipMemcpy(cost.data(), g.d_pixel_cost, cost.size() * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost));
+    std::vector<uint32_t> order(total_blocks);
+    std::vector<uint64_t> bc;
+    const uint32_t head = g.local_tiles * static_cast<uint32_t>(g.nchunks);
+    auto part = [&](uint32_t base, uint32_t nblocks, uint32_t nch) {
+        bc.assign(nblocks, 0);
+        for (uint32_t b = 0; b < nblocks; b++) {
+            const uint32_t lt = b / nch, c = b - lt * nch;
+            const uint32_t s0 = (64u * c) / nch, s1 = (64u * c + 63u) / nch;
+            for (uint32_t sl = s0; sl <= s1 && sl < 64u; sl++) bc[b] += cost[lt * 64u + sl];
+        }
+        std::vector<uint32_t> idx(nblocks);
+        for (uint32_t b = 0; b < nblocks; b++) idx[b] = nblocks - 1u - b;
+        std::stable_sort(idx.begin(), idx.end(),
+                         [&bc](uint32_t x, uint32_t y) { return bc[x] > bc[y]; });
+        for (uint32_t k = 0; k < nblocks; k++) order[base + k] = base + idx[k];
+    };
+    if (head > 0) part(0, head, static_cast<uint32_t>(g.nchunks));
+    if (total_blocks > head)
+        part(head, total_blocks - head, static_cast<uint32_t>(g.tail_nchunks));
+    if (total_blocks > g.order_words) {
+        if (g.d_block_order) (void)hipFree(g.d_block_order);
+        g.d_block_order = nullptr;
+        g.order_words = 0;
+        VCRT_TRY(hipMalloc(&g.d_block_order, total_blocks * sizeof(uint32_t)));
+        g.order_words = total_blocks;
+    }
+    VCRT_TRY(hipMemcpy(g.d_block_order, order.data(), total_blocks * sizeof(uint32_t),
+                       hipMemcpyHostToDevice));
+    return VK_SUCCESS;
 }
 
 vcrt_result vcrt_draw_next_frame(void) {
@@ -1294,6 +1362,42 @@ vcrt_result vcrt_draw_next_frame(void) {
         }
         g.stats.ring_entries = static_cast<int32_t>(p.ring_n);
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
+        // Cost order. When the frame gives each lane of the persistent grid few items, its end
+        // is set by the last expensive items to start (an item's segments run one per wave
+        // iteration: a glass pixel's 16-sample item at depth 8 is ~100 iterations), not by the
+        // work. Then the first frame of a configuration counts each pixel's segments
+        // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
+        // first (TraceParams.block_order). Only the schedule changes: the image depends on the
+        // quantum alone.
+        const uint32_t total_blocks =
+            g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
+        const uint64_t lanes = static_cast<uint64_t>(grid) * block;
+        // (the linear scans only: the flat scans' register budget has no room for the hooks)
+        const bool cost_mode = g.debug_stats == 0 && total_blocks > 0 &&
+                               (kc.f == g.k_trace_smem || kc.f == g.k_trace_lds) &&
+                               (g.cost_order == 1 ||
+                                (g.cost_order < 0 &&
+                                 static_cast<uint64_t>(g.total_items) < kCostOrderItemsPerLane * lanes));
+        const uint64_t key = cost_mode ? order_key_of(kc.f, grid, total_blocks) : 0;
+        bool measure = false;
+        p.pixel_cost = nullptr;
+        p.block_order = nullptr;
+        if (cost_mode && key == g.order_key) {
+            p.block_order = g.d_block_order;
+            p.flags &= ~vcrt::kFlagReverseOrder;  // the order is the whole hand-out sequence
+        } else if (cost_mode) {
+            if (pixels > g.cost_words) {
+                if (g.d_pixel_cost) (void)hipFree(g.d_pixel_cost);
+                g.d_pixel_cost = nullptr;
+                g.cost_words = 0;
+                VCRT_TRY(hipMalloc(&g.d_pixel_cost, pixels * sizeof(uint32_t)));
+                g.cost_words = pixels;
+            }
+            VCRT_TRY(hipMemsetAsync(g.d_pixel_cost, 0, pixels * sizeof(uint32_t), g.stream));
+            p.pixel_cost = g.d_pixel_cost;
+            measure = true;
+        }
+        g.stats.cost_order = p.block_order != nullptr ? 1 : 0;
         VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
         if (g.debug_stats == 1) {  // the stats kernels' region counters, one row per wave
             const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
@@ -1349,6 +1453,11 @@ vcrt_result vcrt_draw_next_frame(void) {
         g.stats.segments = counters[1];
         g.stats.group_tests = counters[2];
         g.stats.bound_tests = counters[3];
+        if (measure) {
+            const VkResult ro = build_block_order(total_blocks);
+            if (ro != VK_SUCCESS) return ro;
+            g.order_key = key;
+        }
         if (g.debug_stats)
             VCRT_TRY(hipMemcpy(g.stats.debug, g.d_debug, sizeof(g.stats.debug),
                                hipMemcpyDeviceToHost));
@@ -1408,6 +1517,8 @@ vcrt_result vcrt_end(void) {
     if (g.d_counters) (void)hipFree(g.d_counters);
     if (g.d_debug) (void)hipFree(g.d_debug);
     if (g.d_region) (void)hipFree(g.d_region);
+    if (g.d_pixel_cost) (void)hipFree(g.d_pixel_cost);
+    if (g.d_block_order) (void)hipFree(g.d_block_order);
     DestroyShaderStage(&g.stage);
     if (g.ev_start) (void)hipEventDestroy(g.ev_start);
     if (g.ev_stop) (void)hipEventDestroy(g.ev_stop);

@@ -1768,6 +1768,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         if (fin) {  // ---- retire the finished quantum: its sum to the pixel ----
             region(rrow, reg::kRetire);
             fin = false;
+            if constexpr (!kFlat) {  // the item's segments (cost order: the linear scans)
+                if (P.pixel_cost != nullptr && need) atomicAdd(P.pixel_cost + (q & kQMask), segs);
+            }
             if ((P.flags & kFlagDirect) != 0u) {
                 // the pixel's one chunk: color /= SPP in fp32 (shader.comp:56)
                 const uint32_t out_index =
@@ -1891,6 +1894,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
                 blk_tail = b >= P.blocks_head;
+                if constexpr (!kFlat) {
+                    if (P.block_order != nullptr) b = P.block_order[b];  // cost order (same part)
+                }
                 if (blk_tail) b -= P.blocks_head;
                 if (reverse) b = (blk_tail ? total_blocks - P.blocks_head : P.blocks_head) - 1u - b;
                 blk_nch = blk_tail ? (uint32_t)P.tail_nchunks : nchunks;
@@ -1977,6 +1983,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             region(rrow, reg::kItem);
             q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
+            if constexpr (!kFlat) {
+                if (P.pixel_cost != nullptr) atomicSub(P.pixel_cost + g_lt * 64u + g_slot, segs);
+            }
             // the item's samples: the four partition values are wave-uniform, read by scalar
             // loads and selected per lane (left to itself the compiler selected their kernarg
             // addresses per lane and read them with vector loads, whose latency the jitter

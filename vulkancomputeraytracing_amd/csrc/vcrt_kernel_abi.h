@@ -110,9 +110,15 @@ struct TraceParams {
     // deferred fetches (the flat scans): a wave whose lanes still have work fetches items only
     // once fetch_min lanes need one or it has deferred fetch_wait iterations (1, 0: every time)
     uint32_t fetch_min, fetch_wait;
-    // stats builds only (VCRT_DEBUG_STATS=1): [waves][72] region entry counts (tracer.hip
+    // stats builds only (VCRT_DEBUG_STATS=1): [waves][88] region entry counts (tracer.hip
     // reg::*), zeroed before the launch; null otherwise
     uint32_t* region;
+    // the cost-ordered schedule (drain-bound frames, capi.cpp "cost order"): pixel_cost, when
+    // set, receives each local pixel's segments (u32, modular: an item subtracts the lane's
+    // segment count at its start and adds it at its end); block_order, when set, maps the k-th
+    // block a part hands out to the block of that part to run (the reverse flag is then off)
+    uint32_t* pixel_cost;
+    const uint32_t* block_order;
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
