@@ -405,7 +405,8 @@ def main():
                        "accumulate_chunk": st["accumulate_chunk"],
                        "accumulate_tail": [st["accumulate_tail"], st["accumulate_tail_chunk"]],
                        "kernel_variant": st["kernel_variant"],
-                       "grid_blocks": st["grid_blocks"]},
+                       "grid_blocks": st["grid_blocks"],
+                       "cost_order": st.get("cost_order", 0)},
             # fp32 VALU-bound (no MFMA). achieved = the fp32 work the timed
             # kernel issued (exact sphere tests and box tests, per-wave counters) / its
             # HIP-event time, so frac <= 1 is a roofline fraction. The brute-force equivalent

@@ -1154,6 +1154,9 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
 // Cost order (vcrt_draw_next_frame): at most this many items per lane of the persistent grid
 // make a frame drain-bound (C2: 3.7; C3, C4 on one GPU: ~100; C4 8-way shards: ~50).
 constexpr uint64_t kCostOrderItemsPerLane = 8;
+// Waves per SIMD of such frames (C2, measured round 5: 0.792 ms at 6 waves, 0.763-0.769 at 5,
+// 0.773 at 4, with the cost order; 0.829 / 0.797 without it).
+constexpr uint32_t kDrainWavesPerSimd = 5;
 
 // The configuration a measured order belongs to: kernel, grid and partition (a new scene or
 // vcrt_begin resets it through order_key = 0).
@@ -1327,6 +1330,27 @@ vcrt_result vcrt_draw_next_frame(void) {
                 per_cu = 1;
             if (g.max_blocks_per_cu > 0) per_cu = std::min(per_cu, g.max_blocks_per_cu);
         }
+        // Cost order. When the frame gives each lane of the persistent grid few items, its end
+        // is set by the last expensive items to start (an item's segments run one per wave
+        // iteration: a glass pixel's 16-sample item at depth 8 is ~100 iterations), not by the
+        // work. Then the first frame of a configuration counts each pixel's segments
+        // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
+        // first (TraceParams.block_order); such frames also run at most kDrainWavesPerSimd
+        // waves per SIMD, so that the waves holding the last items advance faster. Only the
+        // schedule changes: the image depends on the quantum alone. (The linear scans only: the
+        // flat scans' register budget has no room for the hooks.)
+        const uint32_t total_blocks =
+            g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
+        const bool cost_mode =
+            g.debug_stats != 1 && total_blocks > 0 &&
+            (kc.f == g.k_trace_smem || kc.f == g.k_trace_lds) &&
+            (g.cost_order == 1 ||
+             (g.cost_order < 0 &&
+              static_cast<uint64_t>(g.total_items) <
+                  kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block));
+        if (cost_mode && g.desc.blocks_per_cu <= 0 && g.max_blocks_per_cu <= 0)
+            per_cu = std::min(per_cu, std::max(1, static_cast<int>(kDrainWavesPerSimd * 4u * 64u /
+                                                                   block)));
         // The accumulation ring (tracer.hip RingEntry): the LDS the workgroups leave free at
         // this occupancy, up to 63 entries of 32 B per wave, when the frame sums chunk sums
         // (not one chunk per pixel), its blocks are chunk-minor and its pixel indices leave the
@@ -1362,22 +1386,6 @@ vcrt_result vcrt_draw_next_frame(void) {
         }
         g.stats.ring_entries = static_cast<int32_t>(p.ring_n);
         const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
-        // Cost order. When the frame gives each lane of the persistent grid few items, its end
-        // is set by the last expensive items to start (an item's segments run one per wave
-        // iteration: a glass pixel's 16-sample item at depth 8 is ~100 iterations), not by the
-        // work. Then the first frame of a configuration counts each pixel's segments
-        // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
-        // first (TraceParams.block_order). Only the schedule changes: the image depends on the
-        // quantum alone.
-        const uint32_t total_blocks =
-            g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
-        const uint64_t lanes = static_cast<uint64_t>(grid) * block;
-        // (the linear scans only: the flat scans' register budget has no room for the hooks)
-        const bool cost_mode = g.debug_stats == 0 && total_blocks > 0 &&
-                               (kc.f == g.k_trace_smem || kc.f == g.k_trace_lds) &&
-                               (g.cost_order == 1 ||
-                                (g.cost_order < 0 &&
-                                 static_cast<uint64_t>(g.total_items) < kCostOrderItemsPerLane * lanes));
         const uint64_t key = cost_mode ? order_key_of(kc.f, grid, total_blocks) : 0;
         bool measure = false;
         p.pixel_cost = nullptr;
