@@ -1,6 +1,6 @@
 set -o pipefail
-bash tools/gpu_run.sh test || exit 1
-A="--scene three --width 800 --height 450 --spp 64 --depth 8 --frames 40 --rounds 4"
-timeout -k 10 250 python tools/ab.py default default@VCRT_WORK_ORDER=static default@VCRT_MAX_BLOCKS_PER_CU=6 $A > gpurun_out/c2final.json &&
-CFGS=c2 bash tools/gpu_run.sh bench &&
-VCRT_DEBUG_STATS=2 timeout -k 10 100 python tools/wave_times.py ab_objs/wt.hsaco --scene three --width 800 --height 450 --spp 64 --depth 8 --worlds 1 > gpurun_out/wt_c2c.json
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "occupancy_cap or cost_order" > gpurun_out/occ_test.log 2>&1 || { tail -30 gpurun_out/occ_test.log; exit 1; }
+tail -1 gpurun_out/occ_test.log
+timeout -k 10 300 python tools/ab.py default default@VCRT_WORK_ORDER=cost --spp 1024 --rounds 3 --frames 3 > gpurun_out/c4cost.json &&
+timeout -k 10 300 python tools/ab.py default default@VCRT_WORK_ORDER=cost --spp 256 --rounds 4 --frames 4 > gpurun_out/c3cost.json &&
+WORLDS=8 SWEEP_REPS=2 SWEEP_ENVS="VCRT_WORK_ORDER=cost" bash tools/gpu_run.sh sweep
