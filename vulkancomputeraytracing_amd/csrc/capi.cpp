@@ -1356,15 +1356,19 @@ vcrt_result vcrt_draw_next_frame(void) {
         // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
         // first (TraceParams.block_order); such frames also run at most kDrainWavesPerSimd
         // waves per SIMD, so that the waves holding the last items advance faster. Only the
-        // schedule changes: the image depends on the quantum alone. (The flat scans have no
-        // register room for the counting: their measuring frame runs a separate build,
-        // vcrt_trace_cull_flat*_cost.)
+        // schedule changes: the image depends on the quantum alone. Automatic for the linear
+        // scans only: the flat scans' static bottom-up order is already roughly cost-ordered
+        // (sky last) and keeps neighbouring blocks together, and forcing the cost order on them
+        // measured slower (C4 -0.5%, C3 -1.1%, 8-way shards -4%; profiles/r05_ab_log.md). Their
+        // measuring frame runs a separate build (vcrt_trace_cull_flat*_cost): the product
+        // build has no register room for the counting.
         const uint32_t total_blocks =
             g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
+        const bool linear = kc.f == g.k_trace_smem || kc.f == g.k_trace_lds;
         const bool cost_mode =
             g.debug_stats != 1 && total_blocks > 0 && kc.cost != nullptr &&
             (g.cost_order == 1 ||
-             (g.cost_order < 0 &&
+             (g.cost_order < 0 && linear &&
               static_cast<uint64_t>(g.total_items) <
                   kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block));
         if (cost_mode && g.desc.blocks_per_cu <= 0 && g.max_blocks_per_cu <= 0)
