@@ -1,2 +1,2 @@
 set -o pipefail
-timeout -k 10 300 python tools/_tmp_ab_boxes.py 2000 && timeout -k 10 300 python tools/_tmp_ab_boxes.py 1000
+WORLDS=8 SWEEP_REPS=2 SWEEP_ENVS="VCRT_WORK_ORDER=costtail" bash tools/gpu_run.sh sweep
