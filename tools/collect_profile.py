@@ -19,7 +19,6 @@ Derived figures (MI355X_MICROARCH.md rocprofv3 sections):
   valu_lane_util       = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64): active lanes per
                          VALU instruction
 """
-import collections
 import csv
 import json
 import os
@@ -41,21 +40,25 @@ CFG_KEYS = {  # render_once arguments of the PMC passes (tools/gpu_run.sh profil
 
 
 def pmc(name):
+    """Counters of each kernel's last dispatch (the passes render two frames: the second is the
+    steady state, e.g. after the cost order's measuring frame)."""
     path = os.path.join(src, name, "run_counter_collection.csv")
-    agg = collections.defaultdict(float)
-    calls = collections.Counter()
+    last = {}
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"].split("(")[0]
-        agg[(k, r["Counter_Name"])] += float(r["Counter_Value"])
-        calls[(k, r["Counter_Name"])] += 1
-    return {f"{k}|{c}": v / calls[(k, c)] for (k, c), v in agg.items()}  # per dispatch
+        key = (k, r["Counter_Name"])
+        d = int(r["Dispatch_Id"])  # one row per dispatch and counter
+        if key not in last or d > last[key][0]:
+            last[key] = (d, float(r["Counter_Value"]))
+    return {f"{k}|{c}": v for (k, c), (_, v) in last.items()}
 
 
 def run_stats(name):
-    """The render_once JSON (profiled run) printed into the pass's log."""
+    """The render_once JSON (profiled run) printed into the pass's log: its last frame."""
     for line in open(os.path.join(src, name + ".log")):
-        if line.startswith("{"):
-            return json.loads(line)
+        if line.startswith("{") or line.startswith("["):
+            st = json.loads(line)
+            return st[-1] if isinstance(st, list) else st
     raise ValueError(name)
 
 

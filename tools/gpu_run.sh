@@ -121,7 +121,7 @@ mode_profile() {
       > $P/kt_$c.json 2> $P/kt_$c.err) || { tail $P/kt_$c.err; return 1; }
   done
   for c in c4 c3 c2 c5; do
-    local RO=$(cfg_args $c)
+    local RO="$(cfg_args $c) --frames 2"  # the second frame: steady state (collect_profile.py)
     (cd /tmp &&
      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/${c}_fetch -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${c}_fetch.log 2>&1 &&
      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/${c}_write -o run -- python3 $ROOT/tools/render_once.py $RO > $P/${c}_write.log 2>&1 &&
