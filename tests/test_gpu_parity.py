@@ -798,15 +798,13 @@ def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth,
     ("three", 96, 54, 40, 8, vc.KERNEL_SMEM, 0, 0),
     ("three", 37, 23, 48, 8, vc.KERNEL_SMEM, 16, 4),   # ragged edge tiles, a tail part
     ("final", 40, 24, 12, 10, vc.KERNEL_LDS, 0, 0),
-    ("final", 64, 36, 24, 10, vc.KERNEL_CULL_FLAT, 8, 4),     # the flat scan's counting build
-    ("stress4096", 40, 24, 12, 12, vc.KERNEL_CULL_FLAT, 0, 0),  # boxes in LDS, 1024 threads
 ])
 def test_cost_order_bitwise(oracle, monkeypatch, scene, w, h, spp, depth, variant, tail,
                             tail_chunk):
     """The cost-ordered schedule (VCRT_WORK_ORDER=cost; automatic for frames with few items per
     lane): the first frame counts each pixel's segments (TraceParams.pixel_cost), the next hands
     out the blocks most expensive first (block_order). Both frames are the oracle's image. (The
-    flat scans measure with their cost-counting builds, vcrt_trace_cull_flat*_cost.)"""
+    linear scans only: the flat scans keep their static order.)"""
     monkeypatch.setenv("VCRT_WORK_ORDER", "cost")
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
                          kernel_variant=variant, accumulate_tail=tail,

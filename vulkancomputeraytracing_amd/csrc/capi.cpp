@@ -61,10 +61,6 @@ struct RendererState {
                   k_trace_cull_flat_stats = nullptr, k_trace_cull_flat_global = nullptr,
                   k_trace_cull_flat_global_stats = nullptr, k_trace_cull_flat_boxes = nullptr,
                   k_trace_cull_flat_boxes_stats = nullptr, k_setup_jitter = nullptr;
-    // the flat scans' cost-counting builds (the cost order's measuring frame; optional: code
-    // objects built before them lack them, and the flat scans then keep the static order)
-    hipFunction_t k_trace_cull_flat_cost = nullptr, k_trace_cull_flat_global_cost = nullptr,
-                  k_trace_cull_flat_boxes_cost = nullptr;
     // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global, 3 = boxes in LDS (flat scan)
     int cull_lane_tables = 0;
     bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
@@ -473,15 +469,6 @@ VkResult bind_kernels() {
         (void)hipGetLastError();
         g.k_trace_cull_flat_boxes = g.k_trace_cull_flat_boxes_stats = nullptr;
     }
-    for (auto [fp, name] : {std::pair{&g.k_trace_cull_flat_cost, "vcrt_trace_cull_flat_cost"},
-                            std::pair{&g.k_trace_cull_flat_global_cost,
-                                      "vcrt_trace_cull_flat_global_cost"},
-                            std::pair{&g.k_trace_cull_flat_boxes_cost,
-                                      "vcrt_trace_cull_flat_boxes_cost"}})
-        if (hipModuleGetFunction(fp, m, name) != hipSuccess) {
-            (void)hipGetLastError();
-            *fp = nullptr;
-        }
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide, m,
                                   "vcrt_trace_cull_lane_lds_wide"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide_stats, m,
@@ -688,7 +675,7 @@ VkResult wait_gather() {
 // entry point, block size and dynamic LDS.
 struct KernelChoice {
     hipFunction_t f, stats;
-    hipFunction_t cost;  // counts pixel segments (TraceParams.pixel_cost); null: none
+    hipFunction_t cost;  // counts pixel segments (TraceParams.pixel_cost); null: no cost order
     const char* name;
     uint32_t block, lds;
     int variant;
@@ -783,11 +770,8 @@ KernelChoice select_kernel() {
         fs = g.k_trace_cull_lane_stats;
         fname = "vcrt_trace_cull_lane";
     }
-    hipFunction_t fc = f == g.k_trace_smem || f == g.k_trace_lds ? f  // the product counts
-                       : f == g.k_trace_cull_flat                   ? g.k_trace_cull_flat_cost
-                       : f == g.k_trace_cull_flat_global ? g.k_trace_cull_flat_global_cost
-                       : f == g.k_trace_cull_flat_boxes  ? g.k_trace_cull_flat_boxes_cost
-                                                         : nullptr;
+    // the cost order (vcrt_draw_next_frame): the linear scans, whose product builds count
+    hipFunction_t fc = f == g.k_trace_smem || f == g.k_trace_lds ? f : nullptr;
     return KernelChoice{f, fs, fc, fname, block, lds, variant};
 }
 
@@ -1356,19 +1340,17 @@ vcrt_result vcrt_draw_next_frame(void) {
         // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
         // first (TraceParams.block_order); such frames also run at most kDrainWavesPerSimd
         // waves per SIMD, so that the waves holding the last items advance faster. Only the
-        // schedule changes: the image depends on the quantum alone. Automatic for the linear
-        // scans only: the flat scans' static bottom-up order is already roughly cost-ordered
-        // (sky last) and keeps neighbouring blocks together, and forcing the cost order on them
-        // measured slower (C4 -0.5%, C3 -1.1%, 8-way shards -4%; profiles/r05_ab_log.md). Their
-        // measuring frame runs a separate build (vcrt_trace_cull_flat*_cost): the product
-        // build has no register room for the counting.
+        // schedule changes: the image depends on the quantum alone. The linear scans only: the
+        // flat scans' static bottom-up order is already roughly cost-ordered (sky last) and
+        // keeps neighbouring blocks together; the cost order on them (a separate counting build
+        // for the measuring frame) measured slower (C4 -0.5%, C3 -1.1%, 8-way shards -4%;
+        // profiles/r05_ab_log.md), and their product build has no register room for it.
         const uint32_t total_blocks =
             g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
-        const bool linear = kc.f == g.k_trace_smem || kc.f == g.k_trace_lds;
         const bool cost_mode =
             g.debug_stats != 1 && total_blocks > 0 && kc.cost != nullptr &&
             (g.cost_order == 1 ||
-             (g.cost_order < 0 && linear &&
+             (g.cost_order < 0 &&
               static_cast<uint64_t>(g.total_items) <
                   kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block));
         if (cost_mode && g.desc.blocks_per_cu <= 0 && g.max_blocks_per_cu <= 0)
@@ -1451,9 +1433,7 @@ vcrt_result vcrt_draw_next_frame(void) {
                                     g.stream));
         }
         VCRT_TRY(hipEventRecord(g.ev_start, g.stream));
-        // the cost order's measuring frame runs the kernel's cost-counting build (the linear
-        // scans count in their product build)
-        VkResult r = launch(measure ? kc.cost : f, grid, block, lds_launch, p);
+        VkResult r = launch(f, grid, block, lds_launch, p);
         if (r != VK_SUCCESS) return r;
         VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
         if (!g.direct) {

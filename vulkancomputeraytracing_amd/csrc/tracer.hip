@@ -1435,9 +1435,7 @@ __device__ __forceinline__ void shading_rows(const TraceParams& p, const float4*
 
 // kCull: 0 = linear scan (kLds: table in LDS), 1 = culled scan, 2 = per-lane culled scan
 // with the group tables copied to LDS, 3 = per-lane culled scan on global tables.
-// kCost: the flat scans' cost-counting builds (TraceParams.pixel_cost: the measuring frame of
-// the cost order); the linear scans count in their product build.
-template <bool kLds, bool kStats, int kCull = 0, bool kCost = false>
+template <bool kLds, bool kStats, int kCull = 0>
 __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds_dyn) {
     // P: the kernel arguments, read through a pointer to the kernarg segment (the kernels' only
     // argument) that the persistent loop makes opaque at the top of every iteration (below), so
@@ -1770,7 +1768,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         if (fin) {  // ---- retire the finished quantum: its sum to the pixel ----
             region(rrow, reg::kRetire);
             fin = false;
-            if constexpr (!kFlat || kCost) {  // the item's segments (the cost order)
+            if constexpr (!kFlat) {  // the item's segments (the cost order: linear scans)
                 if (P.pixel_cost != nullptr && need) atomicAdd(P.pixel_cost + (q & kQMask), segs);
             }
             if ((P.flags & kFlagDirect) != 0u) {
@@ -1896,8 +1894,10 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
                 blk_tail = b >= P.blocks_head;
-                if (P.block_order != nullptr)  // cost order (same part; a scalar load)
-                    b = ((__attribute__((address_space(4))) const uint32_t*)P.block_order)[b];
+                if constexpr (!kFlat) {  // cost order (same part; a scalar load)
+                    if (P.block_order != nullptr)
+                        b = ((__attribute__((address_space(4))) const uint32_t*)P.block_order)[b];
+                }
                 if (blk_tail) b -= P.blocks_head;
                 if (reverse) b = (blk_tail ? total_blocks - P.blocks_head : P.blocks_head) - 1u - b;
                 blk_nch = blk_tail ? (uint32_t)P.tail_nchunks : nchunks;
@@ -1984,7 +1984,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             region(rrow, reg::kItem);
             q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
-            if constexpr (!kFlat || kCost) {
+            if constexpr (!kFlat) {
                 if (P.pixel_cost != nullptr) atomicSub(P.pixel_cost + g_lt * 64u + g_slot, segs);
             }
             // the item's samples: the four partition values are wave-uniform, read by scalar
@@ -2357,14 +2357,6 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_stats(Tra
     trace_impl<false, true, 4>(p, lds_tab);
 }
 
-// The cost-counting builds of the flat scans (the cost order's measuring frame: each item's
-// segments into TraceParams.pixel_cost), the product's occupancy.
-extern "C" __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_cost(TraceParams p) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-    trace_impl<false, false, 4, true>(p, lds_tab);
-}
-
 #endif
 
 #if !defined(VCRT_PART) || VCRT_PART == 2
@@ -2381,13 +2373,6 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_global_st
     trace_impl<false, true, 5>(p, lds_tab);
 }
 
-extern "C" __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_global_cost(
-    TraceParams p) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-    trace_impl<false, false, 5, true>(p, lds_tab);
-}
-
 // The flat scan for up to 1024 hierarchy groups whose records do not fit in LDS beside the
 // stacks (the stress scene): the group and node boxes in LDS, one copy per CU for 16 waves
 // (1024-thread workgroups), the group records in global memory, 16-bit stack entries.
@@ -2399,11 +2384,6 @@ extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes(Tr
 extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes_stats(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, true, 6>(p, lds_tab);
-}
-
-extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes_cost(TraceParams p) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-    trace_impl<false, false, 6, true>(p, lds_tab);
 }
 
 #endif
