@@ -62,12 +62,14 @@ def parse():
     p.add_argument("--blocks-per-cu", type=int, default=0)
     p.add_argument("--chunk", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--min-warmup-seconds", type=float, default=0.3,
+    p.add_argument("--min-warmup-seconds", type=float, default=3.0,
                    help="after the W warmup steps, further untimed steps until the warmup has "
                         "kept the GPU busy this long: the shader clock follows the load (a lone "
                         "12-ms shard frame runs at ~2.15-2.30 GHz, sustained frames at ~2.38: "
-                        "profiles/r05_clock.txt), and the timed steps measure the steady state. "
-                        "Reported as warmup_extra; 0 turns it off")
+                        "profiles/r05_clock.txt), and the timed steps measure the steady state; "
+                        "3 s also keeps the GPU busy across a once-per-5-s utilisation sampler's "
+                        "tick before the CPU baseline starts. Reported as warmup_extra; 0 turns "
+                        "it off")
     p.add_argument("--validate", action="store_true",
                    help="(the default) after the timed steps, rank 0 checks its frame: bit for "
                         "bit against the CPU oracle on pixels of a few full-width rows at full "
