@@ -221,17 +221,18 @@ def main():
             return "shade(camera phase)." + sh_names.get(r - ev["kShadeBase0"], "?")
         return str(r)
     print(f"stats frame: {st['segments']} segments, {waves} waves, {d[0]} wave-iterations")
-    print(f"{'dynamic VALU':>14} {'share':>6} {'static':>6} {'entries':>12}  region")
+    K = a.kind.upper()
+    print(f"{'dynamic ' + K:>14} {'share':>6} {'static':>6} {'entries':>12}  region")
     for dyn, r, n, cnt in rows:
         name = label(r)
         print(f"{dyn:14.4g} {100 * dyn / total:5.1f}% {n:6d} {cnt:12d}  {name}")
     for want in a.detail:
         for r in static:
             if label(r) == want:
-                print(f"-- {want}: static VALU by innermost source line")
+                print(f"-- {want}: static {K} by innermost source line")
                 for (fl, ln, f), n in sorted(where[r].items()):
                     print(f"   {n:4d}  {fl}:{ln}  {f}")
-    print(f"attributed total {total:.4g} VALU instructions; SQ_INSTS_VALU {a.sq_valu:.4g}: "
+    print(f"attributed total {total:.4g} {K} instructions; SQ_INSTS_{K} {a.sq_valu:.4g}: "
           f"ratio {total / a.sq_valu:.4f}")
     if a.json:
         json.dump({"kernel": a.kernel, "attributed": total, "sq_insts_valu": a.sq_valu,
