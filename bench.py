@@ -317,17 +317,19 @@ def main():
     kernel_ms, segments, gather_ms = [], [], []
     barrier()
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    frame_ms = []
+    for i in range(args.steps):  # per-frame bookkeeping kept light; logged after the timing
         step()
-        st = r.stats()
-        kernel_ms.append(st["kernel_ms"])
-        segments.append(st["segments"])
-        gather_ms.append(st["gather_ms"])
-        log(f"[rank {rank}] step {i}: frame {st['frame_ms']:.1f} ms, kernel "
-            f"{st['kernel_ms']:.1f} ms, gather {st['gather_ms']:.2f} ms, "
-            f"{st['segments']} segments")
+        k, sg, gm, fm = r.frame_times()
+        kernel_ms.append(k)
+        segments.append(sg)
+        gather_ms.append(gm)
+        frame_ms.append(fm)
     barrier()
     elapsed = time.perf_counter() - t0
+    for i in range(args.steps):
+        log(f"[rank {rank}] step {i}: frame {frame_ms[i]:.1f} ms, kernel {kernel_ms[i]:.1f} ms, "
+            f"gather {gather_ms[i]:.2f} ms, {segments[i]} segments")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -173,6 +173,7 @@ class Renderer:
     def __init__(self, desc: RenderDesc | None = None, scene=None):
         self.desc = desc or RenderDesc()
         self._lib = N.lib()
+        self._frame_stats = N.vcrt_stats()  # frame_times()' reused struct
         self._c_desc = self.desc.to_c()
         N.check("vcrt_begin", self._lib.vcrt_begin(ctypes.byref(self._c_desc)))
         self._open = True
@@ -265,6 +266,13 @@ class Renderer:
 
     def shader_load(self, path: str) -> None:
         N.check("vcrt_shader_load", self._lib.vcrt_shader_load(path.encode()))
+
+    def frame_times(self) -> tuple:
+        """(kernel_ms, segments, gather_ms, frame_ms) of the last frame: vcrt_get_stats into a
+        reused struct, without building stats()'s dict (a timed loop's per-frame bookkeeping)."""
+        s = self._frame_stats
+        N.check("vcrt_get_stats", self._lib.vcrt_get_stats(ctypes.byref(s)))
+        return s.kernel_ms, s.segments, s.gather_ms, s.frame_ms
 
     def stats(self) -> dict:
         s = N.vcrt_stats()
