@@ -115,6 +115,9 @@ struct RendererState {
     uint32_t total_pixels = 0, total_items = 0;
     bool direct = false;  // one item per pixel, not progressive: lanes write pixels (kFlagDirect)
     double* d_accum = nullptr;  // [total_pixels][4] exact sums of the quantized chunk sums
+    // d_accum holds zeros: a memset, or the last resolve wrote them back (vcrt_resolve
+    // zero_accum), so a non-progressive frame needs no memset of its own
+    bool accum_clean = false;
     uint64_t accumulated = 0;               // samples per pixel accumulated (progressive)
     // the host's jitter (jx, jy) of a frame's sample indices: two pinned buffers used in turn,
     // each reused only once the copy recorded by its event is done (progressive frames set up
@@ -953,6 +956,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         const size_t bytes = 32u * static_cast<size_t>(g.total_pixels);
         if ((r = to_vk(hipMalloc(&g.d_accum, bytes))) != VK_SUCCESS) return fail(r);
         if ((r = to_vk(hipMemset(g.d_accum, 0, bytes))) != VK_SUCCESS) return fail(r);
+        g.accum_clean = true;
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
     if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e);
@@ -1138,7 +1142,10 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     g.stats.nspheres = count;
     g.accumulated = 0;  // a new scene restarts progressive accumulation
     g.order_key = 0;    // and its cost order is measured again
-    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
+    if (g.d_accum) {
+        VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
+        g.accum_clean = true;
+    }
     g.accum_log2 = scale_log2;
     g.stats.accumulate_scale_log2 = scale_log2;
     g.scene_bounded = true;
@@ -1424,8 +1431,9 @@ vcrt_result vcrt_draw_next_frame(void) {
             VCRT_TRY(hipMemsetAsync(g.d_region, 0, words * sizeof(uint32_t), g.stream));
             p.region = g.d_region;
         }
-        if (!g.direct && !g.desc.progressive)  // every frame sums from zero
+        if (!g.direct && !g.desc.progressive && !g.accum_clean)  // every frame sums from zero
             VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
+        if (!g.direct) g.accum_clean = false;  // until this frame's resolve zeroes it
         if (g.debug_stats) {
             unsigned long long init[128] = {0, 0, 0, 0, 0, ~0ull};
             if (g.debug_stats == 2) init[9] = init[10] = ~0ull;  // wave times: minima
@@ -1446,10 +1454,12 @@ vcrt_result vcrt_draw_next_frame(void) {
                                    g.desc.rank,
                                    g.desc.world_size,
                                    g.tiles_x,
-                                   g.local_tiles};
+                                   g.local_tiles,
+                                   g.desc.progressive ? 0u : 1u};
             const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
             r = launch(g.k_resolve, rgrid, 256, 0, rp);
             if (r != VK_SUCCESS) return r;
+            g.accum_clean = !g.desc.progressive;
             VCRT_TRY(hipEventRecord(g.ev_resolve, g.stream));
         }
         unsigned long long counters[4] = {0, 0, 0, 0};
@@ -1663,7 +1673,10 @@ vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width
 vcrt_result vcrt_reset_accumulation(void) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     VCRT_TRY(hipStreamSynchronize(g.stream));
-    if (g.d_accum) VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
+    if (g.d_accum) {
+        VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
+        g.accum_clean = true;
+    }
     g.accumulated = 0;
     return setup_jitter(0);
 }

@@ -2433,6 +2433,7 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) 
                                   (uint32_t)p.world, (uint32_t)p.rank);
         if (!px.valid) continue;
         const double4 s = *reinterpret_cast<const double4*>(p.accum + 4u * q);
+        if (p.zero_accum) *reinterpret_cast<double4*>(p.accum + 4u * q) = double4{0.0, 0.0, 0.0, 0.0};
         p.out[px.out_index] = make_float4(resolve_channel(s.x, inv, st),
                                           resolve_channel(s.y, inv, st),
                                           resolve_channel(s.z, inv, st),

@@ -165,12 +165,13 @@ struct SetupJitterParams {
 
 // Exact sums -> pixels (vcrt_math.h resolve_channel), rgba32f with alpha 1.
 struct ResolveParams {
-    const double* accum;              // [local_tiles * 64][4]
+    double* accum;                    // [local_tiles * 64][4]
     float4* out;                      // rank-local framebuffer
     double inv_scale;                 // 2^-s (the scale of TraceParams.flags bits 24..31)
     float spp_total;                  // samples per pixel accumulated so far (<= 2^19)
     int32_t width, height, rank, world;
     uint32_t tiles_x, local_tiles;
+    uint32_t zero_accum;  // 1: write zeros back (the next frame sums from zero: no memset)
 };
 
 struct AssembleParams {
