@@ -1879,8 +1879,41 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                         b = kQueues * k + q_x;
                         break;
                     }
+#ifdef VCRT_OLD_DRAIN
                     ++q_drained;
                     q_x = (q_x + 1u) & (kQueues - 1u);
+#else
+                    // this queue is drained: read every queue's counter at once (one load per
+                    // lane; a counter only grows, so "drained" read here is final) and move to
+                    // the next open queue after q_x, or finish when none is open. (Trying the
+                    // queues one atomic at a time made every wave of the grid issue kQueues
+                    // serialized atomics on the same kQueues counters at the end of a frame:
+                    // ~0.25 ms of tail per launch.)
+                    const uint64_t act = __ballot(1);
+                    const uint32_t na = (uint32_t)__popcll(act), rk = lanes_below(act);
+                    uint32_t best = 0u;  // kQueues - (distance of the nearest open queue)
+                    for (uint32_t base = 0; base < kQueues; base += na) {
+                        const uint32_t dq = base + rk + 1u;  // distance from q_x: 1 .. kQueues
+                        uint32_t v = 0u;
+                        if (dq <= kQueues) {
+                            const uint32_t qq = (q_x + dq) & (kQueues - 1u);
+                            const uint32_t cnt = __hip_atomic_load(P.work + kQueueStride * qq,
+                                                                   __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                            const uint32_t nqq = (total_blocks + kQueues - 1u - qq) / kQueues;
+                            if (cnt < nqq) v = kQueues + 1u - dq;
+                        }
+                        best = max(best, wave_max_small<6>(v));
+                    }
+                    // (each failed atomic is on a queue that then reads drained: at most
+                    // kQueues of them per wave, as before)
+                    ++q_drained;
+                    if (best == 0u) {
+                        q_drained = kQueues;
+                    } else {
+                        q_x = (q_x + (kQueues + 1u - best)) & (kQueues - 1u);
+                    }
+#endif
                 }
                 if (b == ~0u) {  // queues drained: lanes still wanting work are done
 #ifdef VCRT_WAVE_END_TIMES
