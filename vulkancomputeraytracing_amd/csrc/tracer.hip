@@ -1865,8 +1865,8 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 if constexpr (kStats && kCull == 0) ++st_fetch;
                 // kQueues queues, each on workgroups of one XCD (workgroups are dispatched to
                 // the XCDs round robin): queue x hands out blocks kQueues k + x on its own
-                // counter; a wave whose queue is drained moves on to the next one, and is done
-                // when it has found every queue drained
+                // counter; a wave whose queue is drained moves on to the next open one, and is
+                // done when it has found every queue drained
                 uint32_t b = ~0u;
                 while (b == ~0u && q_drained < kQueues) {
                     const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
