@@ -70,6 +70,8 @@ def parse():
                         "3 s also keeps the GPU busy across a once-per-5-s utilisation sampler's "
                         "tick before the CPU baseline starts. Reported as warmup_extra; 0 turns "
                         "it off")
+    p.add_argument("--max-warmup-steps", type=int, default=200,
+                   help="upper bound on those extra steps")
     p.add_argument("--validate", action="store_true",
                    help="(the default) after the timed steps, rank 0 checks its frame: bit for "
                         "bit against the CPU oracle on pixels of a few full-width rows at full "
@@ -299,7 +301,7 @@ def main():
         torch.cuda.synchronize()
         frame_s = max(1e-4, (time.perf_counter() - t_w) / args.warmup)
         extra = max(0, int((args.min_warmup_seconds - args.warmup * frame_s) / frame_s + 0.999))
-        extra = min(extra, 200)
+        extra = min(extra, args.max_warmup_steps)
         if world > 1:
             t = torch.tensor([extra], dtype=torch.int64)
             dist.broadcast(t, src=0)
