@@ -794,18 +794,25 @@ def test_accumulation_ring_bitwise(oracle, monkeypatch, scene, w, h, spp, depth,
         assert st["ring_entries"] >= 8
 
 
-@pytest.mark.parametrize("scene,w,h,spp,depth,variant,tail,tail_chunk", [
-    ("three", 96, 54, 40, 8, vc.KERNEL_SMEM, 0, 0),
-    ("three", 37, 23, 48, 8, vc.KERNEL_SMEM, 16, 4),   # ragged edge tiles, a tail part
-    ("final", 40, 24, 12, 10, vc.KERNEL_LDS, 0, 0),
+@pytest.mark.parametrize("scene,w,h,spp,depth,variant,tail,tail_chunk,tables", [
+    ("three", 96, 54, 40, 8, vc.KERNEL_SMEM, 0, 0, ""),
+    ("three", 37, 23, 48, 8, vc.KERNEL_SMEM, 16, 4, ""),   # ragged edge tiles, a tail part
+    ("final", 40, 24, 12, 10, vc.KERNEL_LDS, 0, 0, ""),
+    # the flat scans' cost-order builds: tables in LDS, boxes in LDS, tables in global memory
+    ("final", 40, 24, 12, 10, vc.KERNEL_CULL_FLAT, 0, 0, ""),
+    ("final", 37, 23, 48, 10, vc.KERNEL_CULL_FLAT, 16, 4, ""),
+    ("final", 37, 23, 24, 10, vc.KERNEL_CULL_FLAT, 8, 4, "boxes"),
+    ("final", 37, 23, 24, 10, vc.KERNEL_CULL_FLAT, 0, 0, "global"),
 ])
 def test_cost_order_bitwise(oracle, monkeypatch, scene, w, h, spp, depth, variant, tail,
-                            tail_chunk):
+                            tail_chunk, tables):
     """The cost-ordered schedule (VCRT_WORK_ORDER=cost; automatic for frames with few items per
-    lane): the first frame counts each pixel's segments (TraceParams.pixel_cost), the next hands
-    out the blocks most expensive first (block_order). Both frames are the oracle's image. (The
-    linear scans only: the flat scans keep their static order.)"""
+    lane and for the cost partition): the first frame counts each pixel's segments
+    (TraceParams.pixel_cost), the next hands out the blocks most expensive first (block_order).
+    Both frames are the oracle's image. The flat scans run their cost-order builds."""
     monkeypatch.setenv("VCRT_WORK_ORDER", "cost")
+    if tables:
+        monkeypatch.setenv("VCRT_CULL_LANE_TABLES", tables)
     desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
                          kernel_variant=variant, accumulate_tail=tail,
                          accumulate_tail_chunk=tail_chunk)
@@ -820,6 +827,44 @@ def test_cost_order_bitwise(oracle, monkeypatch, scene, w, h, spp, depth, varian
     assert_bitwise(first, want, f"{scene} measuring frame")
     assert_bitwise(second, want, f"{scene} cost-ordered frame")
     assert st1["segments"] == st2["segments"] == segs
+    flat = {"": "vcrt_trace_cull_flat", "boxes": "vcrt_trace_cull_flat_boxes",
+            "global": "vcrt_trace_cull_flat_global"}
+    if variant == vc.KERNEL_CULL_FLAT:
+        assert st1["kernel"] == st2["kernel"] == flat[tables] + "_cost"
+
+
+@pytest.mark.parametrize("world", [1, 4])
+def test_cost_partition_bitwise(monkeypatch, world):
+    """The cost partition (capi.cpp default_chunk): a frame whose largest rank has few items at
+    the per-pixel rule's K keeps that K, has no tail and runs the cost order (here 48x32 at 1024
+    spp: K = 64, where the item-count rule gives K = 16 and a tail). Every rank's framebuffer, on
+    the measuring frame and the cost-ordered one, equals the static schedule's
+    (VCRT_WORK_ORDER=static: the item-count partition) bit for bit; the image depends on the
+    quantum alone (the static frames are the oracle's: test_bitwise_vs_oracle and the tail tests)."""
+    w, h, spp, depth = 48, 32, 1024, 10
+    for rank in range(world):
+        desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth,
+                             device=0, rank=rank, world_size=world)
+        assert vc.renderer.work_chunk(desc) == 64 and vc.renderer.work_tail(desc) == (0, 0)
+        with vc.Renderer(desc, "final") as r:
+            r.draw_next_frame()
+            first, st1 = r.read_framebuffer(), r.stats()
+            r.draw_next_frame()
+            second, st2 = r.read_framebuffer(), r.stats()
+        assert (st1["cost_order"], st2["cost_order"]) == (0, 1)
+        assert st2["kernel"] == "vcrt_trace_cull_flat_cost"
+        assert (st2["accumulate_chunk"], st2["accumulate_tail"]) == (64, 0)
+        monkeypatch.setenv("VCRT_WORK_ORDER", "static")
+        assert vc.renderer.work_chunk(desc) == 16
+        with vc.Renderer(desc, "final") as r:
+            r.draw_next_frame()
+            want, st = r.read_framebuffer(), r.stats()
+        monkeypatch.delenv("VCRT_WORK_ORDER")
+        assert st["cost_order"] == 0 and st["kernel"] == "vcrt_trace_cull_flat"
+        assert st["accumulate_chunk"] == 16
+        assert_bitwise(first, want, f"rank {rank}/{world} measuring frame")
+        assert_bitwise(second, want, f"rank {rank}/{world} cost-ordered frame")
+        assert st1["segments"] == st2["segments"] == st["segments"]
 
 
 @pytest.mark.parametrize("scene,variant,cap", [("three", vc.KERNEL_SMEM, "3"),

@@ -313,15 +313,30 @@ def _round_up(x, q):
     return -(-x // q) * q
 
 
+def _chunk_rule(slots, spp, cost_ok=True):
+    """capi.cpp default_chunk restated: (K before whole quanta, cost partition). 64, halved down to
+    16 while a pixel has fewer than 16 items; then halved while the largest rank has fewer than
+    2^24 - 2^21 items -- unless the desc may take the cost partition, which keeps the first K (no
+    tail, cost order)."""
+    k_pixel = 64
+    while k_pixel > 16 and spp // k_pixel < 16:
+        k_pixel //= 2
+    k = k_pixel
+    while k > 16 and slots * -(-spp // k) < (1 << 24) - (1 << 21):
+        k //= 2
+    cost = cost_ok and k < k_pixel
+    return (k_pixel if cost else k), cost
+
+
 @pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (37, 23),
                                  (1, 1)])
 @pytest.mark.parametrize("spp", [1, 3, 16, 64, 256, 1024, 4096, 100000])
 def test_work_chunk_rule(w, h, spp):
     """vcrt_work_chunk (the head's samples per work item; host only): the same for every rank of
     a sharded frame, at most spp, whole quanta, and an explicit accumulate_chunk rounded up to
-    whole quanta. Checked against the rule restated here (64, halved while the largest rank has
-    < 2^24 - 2^21 items or a pixel has fewer than 16 items, down to 16; at least spp / 512; then
-    whole quanta)."""
+    whole quanta. Checked against the rule restated here (_chunk_rule; at least spp / 512; then
+    whole quanta), for the default kernel (the cost partition allowed) and for CULL_LANE (no
+    cost-order build: the item-count rule)."""
     q = _quantum_rule(spp)
     for world in (1, 2, 3, 8):
         ks = {vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
@@ -332,11 +347,12 @@ def test_work_chunk_rule(w, h, spp):
         assert 1 <= k <= spp
         assert k == spp or k % q == 0
         slots = 64 * max(len(vc.tiles_for_rank(w, h, world, r)) for r in range(world))
-        want = 64
-        while want > 16 and (slots * -(-spp // want) < (1 << 24) - (1 << 21)
-                             or spp // want < 16):
-            want //= 2
+        want, _ = _chunk_rule(slots, spp)
         assert k == min(_round_up(max(want, -(-spp // 512)), q), spp)
+        want, _ = _chunk_rule(slots, spp, cost_ok=False)
+        assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
+                                                    world_size=world, kernel_variant=4)) \
+            == min(_round_up(max(want, -(-spp // 512)), q), spp)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
                                                     world_size=world, accumulate_chunk=7)) \
             == min(_round_up(7, q), spp)
@@ -345,10 +361,13 @@ def test_work_chunk_rule(w, h, spp):
             accumulate_quantum=1)) == min(7, spp)
     if (w, h, spp) == (1920, 1080, 256):  # C3: K = 16 (16 items per pixel: the ring's reach)
         assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp)) == 16
-    if (w, h, spp) == (1920, 1080, 1024):  # the bench config: K = 64 / 64 / 32 / 16 on 1/2/4/8
-        for world, want in ((1, 64), (2, 64), (4, 32), (8, 16)):
+    if (w, h, spp) == (1920, 1080, 1024):  # the bench config: K = 64 on 1/2/4/8 (4, 8: the cost
+        for world, want in ((1, 64), (2, 64), (4, 64), (8, 64)):  # partition); 64/64/32/16 without
             assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
                                                         world_size=world)) == want
+        for world, want in ((1, 64), (2, 64), (4, 32), (8, 16)):
+            assert vc.renderer.work_chunk(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
+                                                        world_size=world, kernel_variant=4)) == want
 
 
 @pytest.mark.parametrize("w,h", [(1920, 1080), (3840, 2160), (800, 450), (96, 54), (1, 1)])
@@ -356,9 +375,9 @@ def test_work_chunk_rule(w, h, spp):
 def test_work_tail_rule(w, h, spp):
     """vcrt_work_tail (the tail of the work partition; host only): the same for every rank,
     restated here -- T = 6 * K * 327680 / (64 * the largest rank's tiles) to the nearest power of
-    two, none when 4 T > spp or K >= spp or the head has >= 2 (2^24 - 2^21) items, the head ending
-    on a quantum boundary, items of max(4, K / 8) whole quanta -- and explicit values (capped
-    below spp, rounded to whole quanta) or -1 (none)."""
+    two, none when 4 T > spp or K >= spp or the head has >= 2 (2^24 - 2^21) items or the desc takes
+    the cost partition, the head ending on a quantum boundary, items of max(4, K / 8) whole quanta
+    -- and explicit values (capped below spp, rounded to whole quanta) or -1 (none)."""
     import math
     q = _quantum_rule(spp)
     for world in (1, 2, 3, 8):
@@ -373,7 +392,8 @@ def test_work_tail_rule(w, h, spp):
         raw = 6 * 327680 * k / slots
         want = 0
         many = slots * -(-spp // k) >= 2 * ((1 << 24) - (1 << 21))  # the head alone suffices
-        if k < spp and raw >= 1 and not many:
+        _, cost = _chunk_rule(slots, spp)
+        if k < spp and raw >= 1 and not many and not cost:
             want = 1 << round(math.log2(raw))
             if 4 * want > spp:
                 want = 0
@@ -393,9 +413,13 @@ def test_work_tail_rule(w, h, spp):
         d.accumulate_tail = -1
         assert vc.renderer.work_tail(d) == (0, 0)
     if (w, h, spp) == (1920, 1080, 1024):  # the bench config on 1/2/4/8 GPUs
-        for world, want in ((1, (64, 0, 0)), (2, (64, 128, 8)), (4, (32, 128, 4)),
-                            (8, (16, 128, 4))):
+        for world, want in ((1, (64, 0, 0)), (2, (64, 128, 8)), (4, (64, 0, 0)),
+                            (8, (64, 0, 0))):
             d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world)
+            assert (vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d) == want
+        for world, want in ((4, (32, 128, 4)), (8, (16, 128, 4))):  # no cost-order build
+            d = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, world_size=world,
+                              kernel_variant=4)
             assert (vc.renderer.work_chunk(d),) + vc.renderer.work_tail(d) == want
 
 

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -61,6 +62,9 @@ struct RendererState {
                   k_trace_cull_flat_stats = nullptr, k_trace_cull_flat_global = nullptr,
                   k_trace_cull_flat_global_stats = nullptr, k_trace_cull_flat_boxes = nullptr,
                   k_trace_cull_flat_boxes_stats = nullptr, k_setup_jitter = nullptr;
+    // the flat scans' cost-order builds (null: the code object predates them; no cost order)
+    hipFunction_t k_trace_cull_flat_cost = nullptr, k_trace_cull_flat_global_cost = nullptr,
+                  k_trace_cull_flat_boxes_cost = nullptr;
     // VCRT_CULL_LANE_TABLES: 0 = auto, 1 = LDS, 2 = global, 3 = boxes in LDS (flat scan)
     int cull_lane_tables = 0;
     bool accum_ring = true;      // VCRT_ACCUM_RING=0: chunk sums straight to global memory
@@ -71,6 +75,7 @@ struct RendererState {
     // (VCRT_WORK_ORDER=cost / static); the first frame of a configuration measures each pixel's
     // segments, later frames hand out the blocks most expensive first
     int cost_order = -1;
+    bool cost_partition = false;  // the partition is the cost partition (default_chunk)
     uint32_t* d_pixel_cost = nullptr;   // [total_pixels] segments (TraceParams.pixel_cost)
     uint32_t* d_block_order = nullptr;  // [blocks] TraceParams.block_order
     size_t cost_words = 0, order_words = 0;
@@ -183,13 +188,25 @@ constexpr uint64_t kChunkItems = (uint64_t{1} << 24) - (uint64_t{1} << 21);
 // entries (C3: K = 32 gave 9-pixel blocks, and most quanta missed the ring: 2.5 GB of atomics
 // per frame; VCRT_CHUNK_RULE=items restores the item-count rule alone).
 constexpr int32_t kMinChunksPerPixel = 16;
-int32_t default_chunk(uint64_t rank_slots, int32_t spp) {
+// Round 5, the cost partition: where the item count would halve K below the per-pixel rule's K
+// (the 8- and 4-way shards of C4), K stays at the per-pixel rule's value, the partition has no
+// tail and the frame runs the cost order (vcrt_draw_next_frame): the last items of a sharded frame
+// are then cheap ones, not the deep pixels whose 64-sample items outlast the queue by ~3 ms
+// (profiles/r05_ab_log.md: 8-way max rank 11.78 ms against 12.16 with K = 16 + 128 x 4, 4-way
+// 22.94 against 23.11). `allow_cost`: the desc may take it (cost_allowed); `cost` (may be null)
+// reports whether it does.
+int32_t default_chunk(uint64_t rank_slots, int32_t spp, bool allow_cost = false,
+                      bool* cost = nullptr) {
     const char* rule = std::getenv("VCRT_CHUNK_RULE");
     const bool per_pixel = !(rule && std::strcmp(rule, "items") == 0);
     int32_t k = kDefaultChunk;
-    while (k > 16 && (rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems ||
-                      (per_pixel && spp / k < kMinChunksPerPixel)))
-        k /= 2;
+    // the per-pixel rule, then the item-count rule (both conditions are monotone in K)
+    while (k > 16 && per_pixel && spp / k < kMinChunksPerPixel) k /= 2;
+    const int32_t k_pixel = k;
+    while (k > 16 && rank_slots * static_cast<uint64_t>((spp + k - 1) / k) < kChunkItems) k /= 2;
+    const bool c = allow_cost && k < k_pixel;
+    if (cost) *cost = c;
+    if (c) k = k_pixel;
     const int32_t k_min = (spp + vcrt::kAccumMaxChunks - 1) / vcrt::kAccumMaxChunks;
     return std::max(k, k_min);
 }
@@ -264,15 +281,38 @@ int32_t accum_scale_log2(const vcrt_sphere* sp, int32_t n, int32_t depth, int32_
 
 int32_t round_up(int32_t x, int32_t q) { return static_cast<int32_t>((int64_t{x} + q - 1) / q * q); }
 
-// Samples per work item for a desc: its accumulate_chunk, else the default for the largest rank's
-// share of the frame; rounded up to whole quanta and capped at spp.
-int32_t work_chunk(const vcrt_render_desc& d) {
+uint32_t max_rank_tiles(const vcrt_render_desc& d) {
     uint32_t max_tiles = 0;
     for (int32_t rr = 0; rr < d.world_size; rr++)
         max_tiles = std::max(max_tiles, tiles_for_rank(d.width, d.height, d.world_size, rr));
+    return max_tiles;
+}
+
+// Whether a desc may take the cost partition (default_chunk): chunk and tail left to the rules, a
+// kernel variant with a cost-order build (the linear and flat scans; AUTO picks one of them), and
+// no static order asked for (VCRT_WORK_ORDER set to anything but "cost").
+bool cost_allowed(const vcrt_render_desc& d) {
+    if (d.accumulate_chunk > 0 || d.accumulate_tail != 0) return false;
+    if (d.kernel_variant != VCRT_KERNEL_AUTO && d.kernel_variant != VCRT_KERNEL_SMEM &&
+        d.kernel_variant != VCRT_KERNEL_LDS && d.kernel_variant != VCRT_KERNEL_CULL_FLAT)
+        return false;
+    const char* order = std::getenv("VCRT_WORK_ORDER");
+    return !order || std::strcmp(order, "cost") == 0;
+}
+
+bool cost_partition(const vcrt_render_desc& d) {
+    bool cost = false;
+    (void)default_chunk(64ull * max_rank_tiles(d), d.samples_per_pixel, cost_allowed(d), &cost);
+    return cost;
+}
+
+// Samples per work item for a desc: its accumulate_chunk, else the default for the largest rank's
+// share of the frame; rounded up to whole quanta and capped at spp.
+int32_t work_chunk(const vcrt_render_desc& d) {
     const int32_t k = d.accumulate_chunk > 0
                           ? d.accumulate_chunk
-                          : default_chunk(64ull * max_tiles, d.samples_per_pixel);
+                          : default_chunk(64ull * max_rank_tiles(d), d.samples_per_pixel,
+                                          cost_allowed(d));
     return std::min(round_up(k, work_quantum(d)), d.samples_per_pixel);
 }
 
@@ -296,9 +336,8 @@ int32_t work_tail(const vcrt_render_desc& d, int32_t chunk, int32_t* tail_chunk)
     if (d.accumulate_tail > 0) {
         t = std::min(d.accumulate_tail, spp - 1);
     } else {
-        uint32_t max_tiles = 0;
-        for (int32_t rr = 0; rr < d.world_size; rr++)
-            max_tiles = std::max(max_tiles, tiles_for_rank(d.width, d.height, d.world_size, rr));
+        if (cost_partition(d)) return 0;  // the cost order runs the cheap items last instead
+        const uint32_t max_tiles = max_rank_tiles(d);
         // none when the head alone gives every lane many items (>= 2 kChunkItems: ~90 per lane):
         // the drain is then a small part of the frame and the tail's short items cost more than
         // they save. Measured round 5 (tools/ab.py, kernel ms, same bits): one GPU C4 89.68 ->
@@ -472,6 +511,16 @@ VkResult bind_kernels() {
         (void)hipGetLastError();
         g.k_trace_cull_flat_boxes = g.k_trace_cull_flat_boxes_stats = nullptr;
     }
+    // optional as well (A/B builds of earlier trees): the flat scans' cost-order builds
+    const std::pair<hipFunction_t*, const char*> cost_kernels[] = {
+        {&g.k_trace_cull_flat_cost, "vcrt_trace_cull_flat_cost"},
+        {&g.k_trace_cull_flat_global_cost, "vcrt_trace_cull_flat_global_cost"},
+        {&g.k_trace_cull_flat_boxes_cost, "vcrt_trace_cull_flat_boxes_cost"}};
+    for (const auto& [fp, name] : cost_kernels)
+        if (hipModuleGetFunction(fp, m, name) != hipSuccess) {
+            (void)hipGetLastError();
+            *fp = nullptr;
+        }
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide, m,
                                   "vcrt_trace_cull_lane_lds_wide"));
     VCRT_TRY(hipModuleGetFunction(&g.k_trace_cull_lane_lds_wide_stats, m,
@@ -678,7 +727,9 @@ VkResult wait_gather() {
 // entry point, block size and dynamic LDS.
 struct KernelChoice {
     hipFunction_t f, stats;
-    hipFunction_t cost;  // counts pixel segments (TraceParams.pixel_cost); null: no cost order
+    // the build a cost-ordered frame launches (it counts pixel segments into
+    // TraceParams.pixel_cost and follows TraceParams.block_order); null: no cost order
+    hipFunction_t cost;
     const char* name;
     uint32_t block, lds;
     int variant;
@@ -773,8 +824,13 @@ KernelChoice select_kernel() {
         fs = g.k_trace_cull_lane_stats;
         fname = "vcrt_trace_cull_lane";
     }
-    // the cost order (vcrt_draw_next_frame): the linear scans, whose product builds count
-    hipFunction_t fc = f == g.k_trace_smem || f == g.k_trace_lds ? f : nullptr;
+    // the cost order (vcrt_draw_next_frame): the linear scans' product builds have it, the flat
+    // scans have separate builds (the hooks cost the product kernel ~0.3% at C4)
+    hipFunction_t fc = f == g.k_trace_smem || f == g.k_trace_lds        ? f
+                       : f == g.k_trace_cull_flat                        ? g.k_trace_cull_flat_cost
+                       : f == g.k_trace_cull_flat_global ? g.k_trace_cull_flat_global_cost
+                       : f == g.k_trace_cull_flat_boxes  ? g.k_trace_cull_flat_boxes_cost
+                                                         : nullptr;
     return KernelChoice{f, fs, fc, fname, block, lds, variant};
 }
 
@@ -934,6 +990,7 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if ((spp + g.quantum - 1) / g.quantum > vcrt::kAccumMaxChunks)
         return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
     g.chunk = work_chunk(g.desc);
+    g.cost_partition = cost_partition(g.desc);
     {
         const int32_t t = work_tail(g.desc, g.chunk, &g.tail_chunk);
         g.tail_start = spp - t;
@@ -1347,19 +1404,27 @@ vcrt_result vcrt_draw_next_frame(void) {
         // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
         // first (TraceParams.block_order); such frames also run at most kDrainWavesPerSimd
         // waves per SIMD, so that the waves holding the last items advance faster. Only the
-        // schedule changes: the image depends on the quantum alone. The linear scans only: the
-        // flat scans' static bottom-up order is already roughly cost-ordered (sky last) and
-        // keeps neighbouring blocks together; the cost order on them (a separate counting build
-        // for the measuring frame) measured slower (C4 -0.5%, C3 -1.1%, 8-way shards -4%;
-        // profiles/r05_ab_log.md), and their product build has no register room for it.
+        // schedule changes: the image depends on the quantum alone. Automatic for the linear
+        // scans' frames with few items per lane (C2), and for the cost partition (default_chunk:
+        // the 4- and 8-way shards of C4, where the flat scans launch their cost-order builds).
+        // Elsewhere the flat scans' static bottom-up order is already roughly cost-ordered (sky
+        // last) and keeps neighbouring blocks together: the cost order on their own partitions
+        // measured slower (C4 -0.5%, C3 -1.1%, 8-way shards at K = 16 + 128 x 4 -4%;
+        // profiles/r05_ab_log.md).
         const uint32_t total_blocks =
             g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
         const bool cost_mode =
             g.debug_stats != 1 && total_blocks > 0 && kc.cost != nullptr &&
             (g.cost_order == 1 ||
              (g.cost_order < 0 &&
-              static_cast<uint64_t>(g.total_items) <
-                  kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block));
+              (g.cost_partition ||
+               (kc.cost == kc.f &&  // (the linear scans)
+                static_cast<uint64_t>(g.total_items) <
+                    kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block))));
+        if (cost_mode && kc.cost != kc.f) {  // the flat scans' cost-order build
+            f = kc.cost;
+            std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s_cost", kc.name);
+        }
         if (cost_mode && g.desc.blocks_per_cu <= 0 && g.max_blocks_per_cu <= 0)
             per_cu = std::min(per_cu, std::max(1, static_cast<int>(kDrainWavesPerSimd * 4u * 64u /
                                                                    block)));

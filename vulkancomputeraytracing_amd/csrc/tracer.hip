@@ -1435,7 +1435,7 @@ __device__ __forceinline__ void shading_rows(const TraceParams& p, const float4*
 
 // kCull: 0 = linear scan (kLds: table in LDS), 1 = culled scan, 2 = per-lane culled scan
 // with the group tables copied to LDS, 3 = per-lane culled scan on global tables.
-template <bool kLds, bool kStats, int kCull = 0>
+template <bool kLds, bool kStats, int kCull = 0, bool kCostOrder = false>
 __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds_dyn) {
     // P: the kernel arguments, read through a pointer to the kernarg segment (the kernels' only
     // argument) that the persistent loop makes opaque at the top of every iteration (below), so
@@ -1768,7 +1768,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         if (fin) {  // ---- retire the finished quantum: its sum to the pixel ----
             region(rrow, reg::kRetire);
             fin = false;
-            if constexpr (!kFlat) {  // the item's segments (the cost order: linear scans)
+            if constexpr (!kFlat || kCostOrder) {  // the item's segments (the cost order)
                 if (P.pixel_cost != nullptr && need) atomicAdd(P.pixel_cost + (q & kQMask), segs);
             }
             if ((P.flags & kFlagDirect) != 0u) {
@@ -1927,7 +1927,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
                 blk_tail = b >= P.blocks_head;
-                if constexpr (!kFlat) {  // cost order (same part; a scalar load)
+                if constexpr (!kFlat || kCostOrder) {  // cost order (same part; a scalar load)
                     if (P.block_order != nullptr)
                         b = ((__attribute__((address_space(4))) const uint32_t*)P.block_order)[b];
                 }
@@ -2017,7 +2017,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             region(rrow, reg::kItem);
             q = (g_lt * 64u + g_slot) | (g_ent << kRingQBits);
             pxy = (g_py << 16) | g_px;
-            if constexpr (!kFlat) {
+            if constexpr (!kFlat || kCostOrder) {
                 if (P.pixel_cost != nullptr) atomicSub(P.pixel_cost + g_lt * 64u + g_slot, segs);
             }
             // the item's samples: the four partition values are wave-uniform, read by scalar
@@ -2385,6 +2385,14 @@ __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(
     trace_impl<false, false, 4>(p, lds_tab);
 }
 
+// The flat scans' cost-order builds (vcrt_draw_next_frame "cost order"): the product kernel plus
+// the per-pixel segment count of the measuring frame and the block order of later frames.
+extern "C" __global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_cost(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 4, true>(p, lds_tab);
+}
+
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_stats(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, true, 4>(p, lds_tab);
@@ -2401,6 +2409,12 @@ __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_
     trace_impl<false, false, 5>(p, lds_tab);
 }
 
+extern "C" __global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_global_cost(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 5, true>(p, lds_tab);
+}
+
 extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_global_stats(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, true, 5>(p, lds_tab);
@@ -2412,6 +2426,11 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_flat_global_st
 extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, false, 6>(p, lds_tab);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes_cost(TraceParams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+    trace_impl<false, false, 6, true>(p, lds_tab);
 }
 
 extern "C" __global__ __launch_bounds__(1024) void vcrt_trace_cull_flat_boxes_stats(TraceParams p) {
