@@ -92,10 +92,14 @@ typedef struct vcrt_render_desc {
     int32_t world_size;    /* number of shards (GPUs) */
     int32_t kernel_variant;
     int32_t blocks_per_cu; /* persistent grid occupancy; 0 = from the occupancy query */
-    int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 16 while the
-                                 largest rank's share has < 2^24 - 2^21 items: vcrt_work_chunk),
-                                 rounded up to a multiple of the quantum below. A scheduling
-                                 choice only: it does not change the image. */
+    int32_t accumulate_chunk; /* samples per work item (0 = 64, halved down to 16 while a pixel
+                                 has < 16 items, then while the largest rank's share has
+                                 < 2^24 - 2^21 items -- unless the desc takes the cost partition:
+                                 chunk and tail left to the rules and a kernel variant with a
+                                 cost-order build (AUTO, LDS, SMEM, CULL_FLAT), where the second
+                                 halving is skipped, the tail is none and the frames run the cost
+                                 order; vcrt_work_chunk), rounded up to a multiple of the quantum
+                                 below. A scheduling choice only: it does not change the image. */
     int32_t progressive; /* 0: every DrawNextFrame re-renders samples 0..spp-1 (the reference,
                             Linux.cpp:362-366). 1: frame f renders samples f*spp..(f+1)*spp-1 and
                             the framebuffer holds the average of all frames so far (the same
@@ -170,8 +174,9 @@ typedef struct vcrt_stats {
     int32_t accumulate_scale_log2; /* s of the quantization scale 2^s of the quantum sums (per
                                       scene: vcrt_work_scale) */
     int32_t cost_order;            /* 1: the frame's blocks ran most expensive first (the order
-                                      measured by the configuration's first frame; frames with few
-                                      items per lane, or VCRT_WORK_ORDER=cost) */
+                                      measured by the configuration's first frame; the linear
+                                      scans' frames with few items per lane, the cost partition
+                                      (accumulate_chunk), or VCRT_WORK_ORDER=cost) */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
@@ -188,7 +193,8 @@ int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
 /* Tail samples per pixel that vcrt_begin(desc) uses (0: none) and, in *tail_chunk, the samples
  * per tail item; host only. The rule: about six head items per lane of the persistent grid,
  * T = 6 * chunk * 327680 / (64 * the largest rank's tiles) rounded to a power of two, in items
- * of max(4, chunk / 8) samples; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel.
+ * of max(4, chunk / 8) samples; none when 4 T > samples_per_pixel or chunk >= samples_per_pixel,
+ * when the head alone has >= 2 (2^24 - 2^21) items, or for the cost partition (accumulate_chunk).
  * The head ends on a quantum boundary (T is adjusted) and tail items are rounded up to whole
  * quanta. Negative VkResult for an invalid desc. */
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
