@@ -1239,33 +1239,38 @@ uint64_t order_key_of(hipFunction_t f, uint32_t grid, uint32_t total_blocks) {
     return h | 1u;
 }
 
-// From the pixels' segment counts of the frame just rendered: each part's blocks (head, then
-// tail) in decreasing cost, a block's cost being the segments of the pixels its 64 chunk-minor
-// items belong to (item i of tile lt's part with n chunks per pixel: slot i / n); ties in the
-// static order (bottom-up: the highest block first).
+// From the pixels' segment counts of the frame just rendered: every block (head and tail
+// together) by decreasing cost of its items, longest first (the makespan heuristic), so that the
+// items still running when the queue drains are the shortest: the tail's items of cheap pixels.
+// A block's item cost is the mean segment count of the pixels its 64 chunk-minor items belong to
+// (item i of tile lt's part with n chunks per pixel: slot i / n) times the part's samples per
+// item; ties in the static order (head, then tail, each bottom-up: the highest block first).
 VkResult build_block_order(uint32_t total_blocks) {
     std::vector<uint32_t> cost(g.total_pixels);
     VCRT_TRY(hipMemcpy(cost.data(), g.d_pixel_cost, cost.size() * sizeof(uint32_t),
                        hipMemcpyDeviceToHost));
     std::vector<uint32_t> order(total_blocks);
-    std::vector<uint64_t> bc;
+    std::vector<uint64_t> bc(total_blocks, 0);
     const uint32_t head = g.local_tiles * static_cast<uint32_t>(g.nchunks);
-    auto part = [&](uint32_t base, uint32_t nblocks, uint32_t nch) {
-        bc.assign(nblocks, 0);
+    auto part = [&](uint32_t base, uint32_t nblocks, uint32_t nch, uint32_t samples) {
         for (uint32_t b = 0; b < nblocks; b++) {
             const uint32_t lt = b / nch, c = b - lt * nch;
-            const uint32_t s0 = (64u * c) / nch, s1 = (64u * c + 63u) / nch;
-            for (uint32_t sl = s0; sl <= s1 && sl < 64u; sl++) bc[b] += cost[lt * 64u + sl];
+            const uint32_t s0 = (64u * c) / nch, s1 = std::min((64u * c + 63u) / nch, 63u);
+            uint64_t sum = 0;
+            for (uint32_t sl = s0; sl <= s1; sl++) sum += cost[lt * 64u + sl];
+            bc[base + b] = sum * samples * 64u / (s1 - s0 + 1u);
         }
-        std::vector<uint32_t> idx(nblocks);
-        for (uint32_t b = 0; b < nblocks; b++) idx[b] = nblocks - 1u - b;
-        std::stable_sort(idx.begin(), idx.end(),
-                         [&bc](uint32_t x, uint32_t y) { return bc[x] > bc[y]; });
-        for (uint32_t k = 0; k < nblocks; k++) order[base + k] = base + idx[k];
     };
-    if (head > 0) part(0, head, static_cast<uint32_t>(g.nchunks));
+    if (head > 0)
+        part(0, head, static_cast<uint32_t>(g.nchunks), static_cast<uint32_t>(g.chunk));
     if (total_blocks > head)
-        part(head, total_blocks - head, static_cast<uint32_t>(g.tail_nchunks));
+        part(head, total_blocks - head, static_cast<uint32_t>(g.tail_nchunks),
+             static_cast<uint32_t>(g.tail_chunk));
+    uint32_t k = 0;
+    for (uint32_t b = head; b-- > 0;) order[k++] = b;
+    for (uint32_t b = total_blocks; b-- > head;) order[k++] = b;
+    std::stable_sort(order.begin(), order.end(),
+                     [&bc](uint32_t x, uint32_t y) { return bc[x] > bc[y]; });
     if (total_blocks > g.order_words) {
         if (g.d_block_order) (void)hipFree(g.d_block_order);
         g.d_block_order = nullptr;

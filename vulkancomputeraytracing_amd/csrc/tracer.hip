@@ -1926,11 +1926,11 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 region(rrow, reg::kBlock);
                 // block b = (local tile lt, chunk) of the head, then of the tail: wave-uniform
                 // tile origin and sample range; reversed within each part
-                blk_tail = b >= P.blocks_head;
-                if constexpr (!kFlat || kCostOrder) {  // cost order (same part; a scalar load)
+                if constexpr (!kFlat || kCostOrder) {  // cost order (any part; a scalar load)
                     if (P.block_order != nullptr)
                         b = ((__attribute__((address_space(4))) const uint32_t*)P.block_order)[b];
                 }
+                blk_tail = b >= P.blocks_head;
                 if (blk_tail) b -= P.blocks_head;
                 if (reverse) b = (blk_tail ? total_blocks - P.blocks_head : P.blocks_head) - 1u - b;
                 blk_nch = blk_tail ? (uint32_t)P.tail_nchunks : nchunks;
