@@ -1406,8 +1406,8 @@ vcrt_result vcrt_draw_next_frame(void) {
         // is set by the last expensive items to start (an item's segments run one per wave
         // iteration: a glass pixel's 16-sample item at depth 8 is ~100 iterations), not by the
         // work. Then the first frame of a configuration counts each pixel's segments
-        // (TraceParams.pixel_cost), and later frames hand out each part's blocks most expensive
-        // first (TraceParams.block_order); such frames also run at most kDrainWavesPerSimd
+        // (TraceParams.pixel_cost), and later frames hand out the blocks longest items first
+        // (TraceParams.block_order, build_block_order); such frames also run at most kDrainWavesPerSimd
         // waves per SIMD, so that the waves holding the last items advance faster. Only the
         // schedule changes: the image depends on the quantum alone. Automatic for the linear
         // scans' frames with few items per lane (C2), and for the cost partition (default_chunk:
