@@ -361,8 +361,8 @@ def main():
         kernel = st["kernel"]  # the symbol the timed frames launched (vcrt_stats.kernel)
         # Issued work of the timed kernel (the roofline numerator): every lane of each
         # wave-level exact group test (4 spheres x 23 flops, functions.glsl:15-19) and box test
-        # (26 flops), counted by in-kernel per-wave counters; the linear scans issue the
-        # reference's whole scan.
+        # (27 flops, FLOPS_PER_BOUND_TEST), counted by in-kernel per-wave counters; the linear
+        # scans issue the reference's whole scan.
         ref_flops = seg * nspheres * FLOPS_PER_SPHERE_TEST  # brute-force scan, SURVEY.md 8(d)
         issued = ref_flops
         if st["kernel_variant"] in (3, 4, 5):

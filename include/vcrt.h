@@ -121,9 +121,10 @@ typedef struct vcrt_render_desc {
                                    at every progressive frame); when one quantum covers the pixel
                                    (G >= samples_per_pixel, not progressive) the sum is divided in
                                    fp32, the reference's sequential sum (shader.comp:46-56)
-                                   exactly; otherwise every quantum sum is quantized to 2^-s (s:
-                                   vcrt_work_scale, 32 for the reference scenes) and added
-                                   exactly. So the image depends on G (and the scene's s) only -- not on the
+                                   exactly; otherwise every quantum sum is quantized to 2^-s (s per
+                                   pixel from its own quantum sums: vcrt_pixel_scale_log2, 32 for
+                                   every pixel of the reference scenes) and added exactly. So the
+                                   image depends on G only -- not on the
                                    work items, the schedule or the number of GPUs: a sharded frame
                                    equals a one-GPU render bit for bit. Work items hold whole
                                    quanta. At most 512 quanta per pixel (progressive frames
@@ -171,12 +172,17 @@ typedef struct vcrt_stats {
     int32_t ring_entries;          /* LDS accumulation ring entries per wave (0: none; the chunk
                                       sums go to global memory directly) */
     int32_t accumulate_quantum;    /* the accumulation quantum G in effect */
-    int32_t accumulate_scale_log2; /* s of the quantization scale 2^s of the quantum sums (per
-                                      scene: vcrt_work_scale) */
+    int32_t accumulate_scale_log2; /* the smallest per-pixel quantization scale s of the frame
+                                      (vcrt_pixel_scale_log2): 32 unless some pixel's quantum
+                                      sums reach 2^12 in magnitude */
     int32_t cost_order;            /* 1: the frame's blocks ran most expensive first (the order
                                       measured by the configuration's first frame; the linear
                                       scans' frames with few items per lane, the cost partition
                                       (accumulate_chunk), or VCRT_WORK_ORDER=cost) */
+    int32_t scale_rerenders;       /* renders the last vcrt_draw_next_frame added because a
+                                      pixel's quantum sums first reached 2^12 (its scale below 32:
+                                      the frame -- progressive: every frame so far -- is rendered
+                                      again with each pixel at its own scale) */
 } vcrt_stats;
 
 /* Fills *desc with the reference defaults: 1280x720, 1 spp, depth 50, camera
@@ -198,14 +204,14 @@ int32_t vcrt_work_chunk(const vcrt_render_desc* desc);
  * The head ends on a quantum boundary (T is adjusted) and tail items are rounded up to whole
  * quanta. Negative VkResult for an invalid desc. */
 int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk);
-/* The quantization scale 2^s of the quantum sums for a scene under desc (host only): the
- * largest s <= 32 with G * R * 2^s < 2^44, where G is the quantum and R = A^max_depth bounds one
- * sample's radiance, A the scene's largest per-bounce attenuation (Lambertian albedo * param,
- * metal albedo; at least 1). So every finite quantum sum is held exactly, whatever the scene;
- * the reference scenes take s = 32. One quantum per pixel: 32 (no quantization). Returns
- * VCRT_ERROR_FORMAT_NOT_SUPPORTED when no scale holds the scene (R > 2^120). */
-vcrt_result vcrt_work_scale(const vcrt_render_desc* desc, const vcrt_sphere* spheres,
-                            int32_t count, int32_t* scale_log2);
+/* The quantization scale 2^s of a pixel's quantum sums (host only), from E = the largest |S| of
+ * its finite quantum sums over every channel (and every progressive frame so far): 32 while
+ * E < 2^12 (every pixel of the reference scenes, radiance <= 1 per sample), else the largest s
+ * with E * 2^s < 2^44 = 43 - floor(log2 E). Each quantized sum is then an integer below 2^44 and
+ * a pixel's (at most 512) of them add exactly in double, whatever the scene's brightness. The
+ * renderer measures E while it renders: a frame where some pixel first needs s < 32 is
+ * rendered again with every pixel at its own scale (vcrt_stats.scale_rerenders). */
+int32_t vcrt_pixel_scale_log2(float max_abs_quantum_sum);
 /* Uploads the scene and builds, on the host, its culling tables and the camera-ray lists for
  * this desc's camera and shard (vcrt_cull_tables, vcrt_primary_lists: ~0.1 s for the final
  * scene at 1080p, ~0.4 s for 4100 spheres at 4K). vcrt_begin sets the final scene. */

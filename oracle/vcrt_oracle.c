@@ -335,6 +335,7 @@ typedef struct {
     const oracle_sphere* world;
     int n;
     float* rgba;
+    float* seq_rgba; /* optional: the reference's sequential fp32 sum / spp per pixel */
     const float* jitter; /* 2*spp: (-0.5+rand(i,i), -0.5+rand(i+1,i+1)) */
     float cam[15];
     int32_t row_begin, row_end, row_step, nrows;
@@ -343,52 +344,34 @@ typedef struct {
     volatile int next; /* row (or pixel-batch) counter */
     pthread_mutex_t lock;
     uint64_t segments;
-    int32_t scale_log2; /* the quantization scale 2^s of the quantum sums (oracle_scale_log2) */
+    int failed;
 } render_job;
 
-/* The quantization scale 2^s of the quantum sums (vulkancomputeraytracing_amd/csrc/vcrt_math.h
- * "Accumulation", restated from the rule, not shared code): one sample's radiance is the sky's
- * factor (functions.glsl:86-88, <= 1) times the attenuation of each bounce -- albedo * param for
- * Lambertian (textures.glsl:22), albedo for metal (:60), 1 for glass (:27-56) -- so its magnitude
- * is at most R = A^depth, A = max(1, the scene's largest factor). A run of G samples sums to at
- * most G R; s is the largest integer <= 32 with G R 2^s < 2^44 (slack factors for the fp32
- * roundings: two per bounce, the sky's mix, the run's additions). Material ids convert like the
- * kernel's (int) of texture.x; ids out of int range (or NaN) count as both Lambertian and metal;
- * non-finite factors are left out (they only make radiance non-finite: a NaN pixel). Returns
- * INT32_MIN when no s >= -80 holds the scene. */
-int32_t oracle_scale_log2(const oracle_sphere* world, int32_t n, int32_t max_depth,
-                          int32_t quantum) {
-    double a = 1.0;
-    for (int32_t i = 0; i < n; i++) {
-        const float id = world[i].texture[0];
-        const int known = fabsf(id) < 2147483648.0f;
-        const int t = known ? (int)id : 0;
-        for (int c = 0; c < 3; c++) {
-            const double col = fabs((double)world[i].colour[c]);
-            const double f = col * fabs((double)world[i].texture[1]);
-            if ((!known || t == 1) && isfinite(f) && f > a) a = f;
-            if ((!known || t == 2) && isfinite(col) && col > a) a = col;
-        }
-    }
-    const double r = pow(a * (1.0 + 0x1p-22), max_depth > 1 ? max_depth : 1) * (1.0 + 0x1p-20) *
-                     (double)quantum * (1.0 + (double)quantum * 0x1p-23);
-    if (!(r < 0x1p120)) return INT32_MIN;
-    int32_t sc = 32;
-    while (sc > -80 && ldexp(r, sc) >= 0x1p44) sc--;
-    return ldexp(r, sc) < 0x1p44 ? sc : INT32_MIN;
+/* The quantization scale 2^s of one pixel's run sums (vulkancomputeraytracing_amd/csrc/
+ * vcrt_math.h "Accumulation", restated from the rule, not shared code): E = the largest |S| over
+ * the channels of the pixel's finite run sums (all progressive frames so far); s = 32 while
+ * E < 2^12, else s = 43 - floor(log2 E), the largest s with E * 2^s < 2^44. Every quantized run
+ * sum is then an integer below 2^44 and the pixel's at most 512 of them add exactly in double. */
+int32_t oracle_pixel_scale_log2(float max_abs) {
+    max_abs = fabsf(max_abs);
+    if (!(max_abs >= 0x1p12f) || isinf(max_abs)) return 32; /* (only finite sums count) */
+    int e;
+    (void)frexpf(max_abs, &e); /* max_abs = m * 2^e, m in [0.5, 1): floor(log2) = e - 1 */
+    return 43 - (e - 1);
 }
 
-/* One pixel (shader.comp:43-57) into px[4]. Accumulation (vulkancomputeraytracing_amd/csrc/
- * vcrt_math.h "Accumulation"): the samples are cut into quanta of G (accumulate_quantum; before
- * round 4, and still when it is 0, chunks of K plus the tail's chunks), restarting at every
- * progressive frame of frame_spp samples; a quantum is summed in fp32 in sample order, as the
- * reference sums (shader.comp:46-54). A single chunk (K >= spp, no progressive frames) is then
- * divided by SAMPLES_PER_PIXEL in fp32: the reference's own arithmetic (shader.comp:56).
- * Otherwise every quantum sum S is quantized to q = RN_even(S * 2^s) with the scene's scale
- * (oracle_scale_log2; |S * 2^s| < 2^44, a NaN, infinite or larger scaled sum makes the pixel
- * NaN), the q are added exactly (integers below 2^53 in double), and the pixel is
- * (float)((sum * 2^-s) / spp). */
-static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* segs) {
+/* One pixel (shader.comp:43-57) into px[4] (and the sequential sum into seq[4] if given).
+ * Accumulation (vulkancomputeraytracing_amd/csrc/vcrt_math.h "Accumulation"): the samples are
+ * cut into quanta of G (accumulate_quantum; before round 4, and still when it is 0, chunks of K
+ * plus the tail's chunks), restarting at every progressive frame of frame_spp samples; a quantum
+ * is summed in fp32 in sample order, as the reference sums (shader.comp:46-54). A single chunk
+ * (K >= spp, no progressive frames) is then divided by SAMPLES_PER_PIXEL in fp32: the
+ * reference's own arithmetic (shader.comp:56). Otherwise every quantum sum S is quantized to
+ * q = RN_even(S * 2^s) with the pixel's scale (oracle_pixel_scale_log2; a NaN or infinite sum
+ * makes the pixel NaN), the q are added exactly (integers below 2^53 in double), and the pixel
+ * is (float)((sum * 2^-s) / spp). runs: scratch for 3 floats per run (at most spp runs). */
+static void render_pixel(render_job* job, int x, int y, float* px, float* seq, float* runs,
+                         uint64_t* segs) {
     const oracle_config* cfg = job->cfg;
     v3 p00 = V(job->cam[0], job->cam[1], job->cam[2]);
     v3 du = V(job->cam[3], job->cam[4], job->cam[5]);
@@ -414,8 +397,10 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
     const int quantum = cfg->accumulate_quantum;
     const int single = quantum > 0 ? (cfg->frame_spp <= 0 && quantum >= cfg->spp)
                                    : (cfg->frame_spp <= 0 && chunk >= cfg->spp && tail == 0);
-    double sum[3] = {0.0, 0.0, 0.0};
     v3 part = V(0.0f, 0.0f, 0.0f);
+    v3 all = V(0.0f, 0.0f, 0.0f); /* the sequential sum (shader.comp:53) */
+    int nruns = 0, nan = 0;
+    float emax = 0.0f;
     for (int c0 = 0; c0 < cfg->spp;) {
         part = V(0.0f, 0.0f, 0.0f);
         int block_end = (c0 / block + 1) * block;
@@ -433,28 +418,44 @@ static void render_pixel(render_job* job, int x, int y, float* px, uint64_t* seg
             v3 rs = vadd(vscale(jx, du), vscale(jy, dv));
             v3 ps = vadd(pc, rs);
             v3 dir = vsub(ps, center);
-            part = vadd(part, ray_color(job->world, job->n, center, dir, cfg->max_depth, segs));
+            const v3 rc = ray_color(job->world, job->n, center, dir, cfg->max_depth, segs);
+            part = vadd(part, rc);
+            all = vadd(all, rc);
         }
-        const float sc = ldexpf(1.0f, job->scale_log2);
-        const float qx = part.x * sc, qy = part.y * sc, qz = part.z * sc;
-        if (!(fabsf(qx) < 0x1p44f && fabsf(qy) < 0x1p44f && fabsf(qz) < 0x1p44f)) {
-            sum[0] = sum[1] = sum[2] = NAN; /* NaN stays NaN through later additions */
+        if (!(isfinite(part.x) && isfinite(part.y) && isfinite(part.z))) {
+            nan = 1; /* NaN stays NaN through later additions */
         } else {
-            sum[0] += (double)rintf(qx);
-            sum[1] += (double)rintf(qy);
-            sum[2] += (double)rintf(qz);
+            const float m = fmaxf(fabsf(part.x), fmaxf(fabsf(part.y), fabsf(part.z)));
+            if (m > emax) emax = m;
         }
+        runs[3 * nruns + 0] = part.x;
+        runs[3 * nruns + 1] = part.y;
+        runs[3 * nruns + 2] = part.z;
+        nruns++;
         c0 = c1;
     }
     if (single) { /* color /= SAMPLES_PER_PIXEL in fp32 (shader.comp:56) */
         px[0] = part.x / (float)cfg->spp;
         px[1] = part.y / (float)cfg->spp;
         px[2] = part.z / (float)cfg->spp;
+    } else if (nan) {
+        px[0] = px[1] = px[2] = NAN;
     } else {
+        const int32_t s = oracle_pixel_scale_log2(emax);
+        const float sc = ldexpf(1.0f, s);
+        double sum[3] = {0.0, 0.0, 0.0};
+        for (int r = 0; r < nruns; r++)
+            for (int k = 0; k < 3; k++) sum[k] += (double)rintf(runs[3 * r + k] * sc);
         for (int k = 0; k < 3; k++)
-            px[k] = (float)((sum[k] * ldexp(1.0, -job->scale_log2)) / (double)cfg->spp);
+            px[k] = (float)((sum[k] * ldexp(1.0, -s)) / (double)cfg->spp);
     }
     px[3] = 1.0f;
+    if (seq) {
+        seq[0] = all.x / (float)cfg->spp;
+        seq[1] = all.y / (float)cfg->spp;
+        seq[2] = all.z / (float)cfg->spp;
+        seq[3] = 1.0f;
+    }
 }
 
 static void* render_worker(void* arg) {
@@ -463,6 +464,13 @@ static void* render_worker(void* arg) {
     uint64_t segs = 0;
     const int batch = 16; /* pixel-list mode hands out pixels 16 at a time */
     const int units = job->pixels ? (job->npixels + batch - 1) / batch : job->nrows;
+    float* runs = (float*)malloc(sizeof(float) * 3 * (size_t)cfg->spp);
+    if (!runs) {
+        pthread_mutex_lock(&job->lock);
+        job->failed = 1;
+        pthread_mutex_unlock(&job->lock);
+        return NULL;
+    }
     for (;;) {
         pthread_mutex_lock(&job->lock);
         int k = job->next++;
@@ -471,34 +479,25 @@ static void* render_worker(void* arg) {
         if (job->pixels) {
             for (int p = k * batch; p < job->npixels && p < (k + 1) * batch; p++)
                 render_pixel(job, job->pixels[2 * p], job->pixels[2 * p + 1], job->rgba + 4 * p,
-                             &segs);
+                             job->seq_rgba ? job->seq_rgba + 4 * p : NULL, runs, &segs);
         } else {
             int y = job->row_begin + k * job->row_step;
-            for (int x = 0; x < cfg->width; x++)
-                render_pixel(job, x, y, job->rgba + ((size_t)y * cfg->width + x) * 4, &segs);
+            for (int x = 0; x < cfg->width; x++) {
+                const size_t o = ((size_t)y * cfg->width + x) * 4;
+                render_pixel(job, x, y, job->rgba + o, job->seq_rgba ? job->seq_rgba + o : NULL,
+                             runs, &segs);
+            }
         }
     }
+    free(runs);
     pthread_mutex_lock(&job->lock);
     job->segments += segs;
     pthread_mutex_unlock(&job->lock);
     return NULL;
 }
 
-/* The longest run of samples summed in fp32 before quantization (the G of oracle_scale_log2). */
-static int32_t run_length(const oracle_config* cfg) {
-    if (cfg->accumulate_quantum > 0) return cfg->accumulate_quantum;
-    const int32_t block = (cfg->frame_spp <= 0 || cfg->frame_spp > cfg->spp) ? cfg->spp
-                                                                            : cfg->frame_spp;
-    int32_t g = (cfg->accumulate_chunk <= 0 || cfg->accumulate_chunk >= block)
-                    ? block : cfg->accumulate_chunk;
-    if (cfg->accumulate_tail_chunk > g) g = cfg->accumulate_tail_chunk;
-    return g;
-}
-
 static int run_job(render_job* job, int32_t threads, uint64_t* segments) {
     const oracle_config* cfg = job->cfg;
-    job->scale_log2 = oracle_scale_log2(job->world, job->n, cfg->max_depth, run_length(cfg));
-    if (job->scale_log2 == INT32_MIN) return -1;
     oracle_camera(cfg, job->cam);
     float* jit = (float*)malloc(sizeof(float) * 2 * (size_t)cfg->spp);
     if (!jit) return -1;
@@ -521,6 +520,7 @@ static int run_job(render_job* job, int32_t threads, uint64_t* segments) {
     }
     pthread_mutex_destroy(&job->lock);
     free(jit);
+    if (job->failed) return -1;
     if (segments) *segments = job->segments;
     return 0;
 }
@@ -532,6 +532,13 @@ static int config_ok(const oracle_config* cfg) {
 int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t n, float* rgba,
                   int32_t row_begin, int32_t row_end, int32_t row_step, int32_t threads,
                   uint64_t* segments) {
+    return oracle_render_seq(cfg, world, n, rgba, NULL, row_begin, row_end, row_step, threads,
+                             segments);
+}
+
+int oracle_render_seq(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
+                      float* rgba, float* seq_rgba, int32_t row_begin, int32_t row_end,
+                      int32_t row_step, int32_t threads, uint64_t* segments) {
     if (!config_ok(cfg) || !rgba || n < 0 || (n > 0 && !world)) return -1;
     if (row_step <= 0) row_step = 1;
     if (row_begin < 0) row_begin = 0;
@@ -542,6 +549,7 @@ int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t 
     job.world = world;
     job.n = n;
     job.rgba = rgba;
+    job.seq_rgba = seq_rgba;
     job.row_begin = row_begin;
     job.row_end = row_end;
     job.row_step = row_step;
@@ -552,6 +560,12 @@ int oracle_render(const oracle_config* cfg, const oracle_sphere* world, int32_t 
 int oracle_render_pixels(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
                          const int32_t* xy, int32_t npixels, float* rgba, int32_t threads,
                          uint64_t* segments) {
+    return oracle_render_pixels_seq(cfg, world, n, xy, npixels, rgba, NULL, threads, segments);
+}
+
+int oracle_render_pixels_seq(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
+                             const int32_t* xy, int32_t npixels, float* rgba, float* seq_rgba,
+                             int32_t threads, uint64_t* segments) {
     if (!config_ok(cfg) || npixels < 0 || (npixels > 0 && (!xy || !rgba)) || n < 0 ||
         (n > 0 && !world))
         return -1;
@@ -565,6 +579,7 @@ int oracle_render_pixels(const oracle_config* cfg, const oracle_sphere* world, i
     job.world = world;
     job.n = n;
     job.rgba = rgba;
+    job.seq_rgba = seq_rgba;
     job.pixels = xy;
     job.npixels = npixels;
     return run_job(&job, threads, segments);

@@ -77,11 +77,19 @@ int oracle_render_pixels(const oracle_config* cfg, const oracle_sphere* world, i
                          const int32_t* xy, int32_t npixels, float* rgba, int32_t threads,
                          uint64_t* segments);
 
-/* The quantization scale 2^s of the quantum sums for a scene, depth and quantum G (the largest
- * s <= 32 with G * A^depth * 2^s < 2^44, A the largest per-bounce attenuation, >= 1; see
- * vcrt_oracle.c). INT32_MIN when no scale holds the scene (oracle_render then returns -1). */
-int32_t oracle_scale_log2(const oracle_sphere* world, int32_t n, int32_t max_depth,
-                          int32_t quantum);
+/* The same two renders, with the reference's sequential fp32 sum / spp of every rendered pixel
+ * (shader.comp:46-56, one chunk) written to seq_rgba beside the accumulated rgba: one pass. */
+int oracle_render_seq(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
+                      float* rgba, float* seq_rgba, int32_t row_begin, int32_t row_end,
+                      int32_t row_step, int32_t threads, uint64_t* segments);
+int oracle_render_pixels_seq(const oracle_config* cfg, const oracle_sphere* world, int32_t n,
+                             const int32_t* xy, int32_t npixels, float* rgba, float* seq_rgba,
+                             int32_t threads, uint64_t* segments);
+
+/* The quantization scale 2^s of a pixel's quantum sums from the largest |S| among them (all
+ * channels, finite sums only): 32 while it is below 2^12, else the largest s with
+ * |S| * 2^s < 2^44 (see vcrt_oracle.c). */
+int32_t oracle_pixel_scale_log2(float max_abs);
 
 /* Per-pixel radiance of one sample (ray_color), for KATs. */
 void oracle_ray_color(const oracle_sphere* world, int32_t n, const float origin[3],

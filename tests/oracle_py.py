@@ -73,9 +73,18 @@ class Oracle:
         L.oracle_scene_generator_text.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_reference_constants.restype = None
         L.oracle_reference_constants.argtypes = [ctypes.c_void_p]
-        L.oracle_scale_log2.restype = ctypes.c_int32
-        L.oracle_scale_log2.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
-                                        ctypes.c_int32]
+        L.oracle_pixel_scale_log2.restype = ctypes.c_int32
+        L.oracle_pixel_scale_log2.argtypes = [ctypes.c_float]
+        L.oracle_render_seq.restype = ctypes.c_int
+        L.oracle_render_seq.argtypes = [ctypes.POINTER(OracleConfig), ctypes.c_void_p,
+                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_render_pixels_seq.restype = ctypes.c_int
+        L.oracle_render_pixels_seq.argtypes = [ctypes.POINTER(OracleConfig), ctypes.c_void_p,
+                                               ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                               ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_scene_random_spheres.restype = ctypes.c_int32
         L.oracle_scene_random_spheres.argtypes = [ctypes.c_int32] * 3 + [ctypes.c_void_p,
                                                                          ctypes.c_int32]
@@ -127,11 +136,10 @@ class Oracle:
                     tail_chunk=stats["accumulate_tail_chunk"],
                     quantum=stats["accumulate_quantum"])
 
-    def scale_log2(self, spheres, max_depth: int, quantum: int) -> int:
-        """s of the quantization scale 2^s of the quantum sums (oracle_scale_log2);
-        -2**31 when no scale holds the scene."""
-        spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
-        return self.lib.oracle_scale_log2(spheres.ctypes.data, len(spheres), max_depth, quantum)
+    def pixel_scale_log2(self, max_abs: float) -> int:
+        """s of a pixel's quantization scale 2^s from its largest |quantum sum|
+        (oracle_pixel_scale_log2)."""
+        return self.lib.oracle_pixel_scale_log2(max_abs)
 
     # ---- render ----
     def render(self, cfg: OracleConfig, spheres: np.ndarray, rows=None, threads: int = 0):
@@ -150,6 +158,41 @@ class Oracle:
         if r != 0:
             raise ValueError("oracle_render rejected its arguments")
         return img, segs.value
+
+    def render_seq(self, cfg: OracleConfig, spheres: np.ndarray, rows=None, threads: int = 0):
+        """render() plus the reference's sequential fp32 sum / spp of the same rows, in one pass:
+        (image, sequential image, segments)."""
+        spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+        img = np.zeros((cfg.height, cfg.width, 4), dtype=np.float32)
+        seq = np.zeros_like(img)
+        if rows is None:
+            rows = range(0, cfg.height, 1)
+        if threads <= 0:
+            threads = min(os.cpu_count() or 1, 16)
+        segs = ctypes.c_uint64()
+        r = self.lib.oracle_render_seq(ctypes.byref(cfg), spheres.ctypes.data, len(spheres),
+                                       img.ctypes.data, seq.ctypes.data, rows.start, rows.stop,
+                                       rows.step or 1, threads, ctypes.byref(segs))
+        if r != 0:
+            raise ValueError("oracle_render_seq rejected its arguments")
+        return img, seq, segs.value
+
+    def render_pixels_seq(self, cfg: OracleConfig, spheres: np.ndarray, xy, threads: int = 0):
+        """render_pixels() plus the sequential fp32 sum / spp: (rgba, sequential, segments)."""
+        spheres = np.ascontiguousarray(spheres, dtype=SPHERE_DTYPE)
+        xy = np.ascontiguousarray(np.asarray(xy, dtype=np.int32).reshape(-1, 2))
+        out = np.zeros((len(xy), 4), dtype=np.float32)
+        seq = np.zeros_like(out)
+        if threads <= 0:
+            threads = min(os.cpu_count() or 1, 16)
+        segs = ctypes.c_uint64()
+        r = self.lib.oracle_render_pixels_seq(ctypes.byref(cfg), spheres.ctypes.data,
+                                              len(spheres), xy.ctypes.data, len(xy),
+                                              out.ctypes.data, seq.ctypes.data, threads,
+                                              ctypes.byref(segs))
+        if r != 0:
+            raise ValueError("oracle_render_pixels_seq rejected its arguments")
+        return out, seq, segs.value
 
     def render_pixels(self, cfg: OracleConfig, spheres: np.ndarray, xy, threads: int = 0):
         """Pixels xy [(x, y), ...] of a W x H frame -> (float32 [len(xy), 4], segments)."""

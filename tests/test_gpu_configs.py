@@ -1,19 +1,26 @@
 """GPU parity at BASELINE.json's own workloads (configs C1-C5 at their exact width x height,
 samples per pixel, depth and scene), through the C ABI, against the CPU oracle.
 
-The HIP path renders every config's full frame. The oracle (a linear scan in C) cannot render
-a 1024-spp 1080p frame in seconds, so each config is compared on a subset the CPU affords, at
-the config's full spp and depth:
-  C1  256x144, 1 spp, depth 1, red scene          whole frame
-  C2  800x450, 64 spp, depth 8, three-material     whole frame
-  C3  1920x1080, 256 spp, depth 10, final scene    8 rows spread over the frame
-  C4  1920x1080, 1024 spp, depth 10, final scene   8 rows; also sharded 8 ways
-  C5  3840x2160, 4096 spp, depth 50, 4100 spheres  64 pixels on an 8x8 grid
+The HIP path renders every config's full frame, compared with the oracle at the config's full
+spp and depth:
+  C1  256x144, 1 spp, depth 1, red scene          whole frame (oracle run in the test)
+  C2  800x450, 64 spp, depth 8, three-material     whole frame (oracle run in the test)
+  C3  1920x1080, 256 spp, depth 10, final scene    whole frame: sha256 of every pixel's bits, per
+                                                   row and whole, and the segment total, against
+                                                   tests/golden/full_frame_digests.json (the
+                                                   oracle over the entire frame, made in the
+                                                   build container); plus 8 rows run here
+  C4  1920x1080, 1024 spp, depth 10, final scene   the same whole-frame digests, also for the
+                                                   8-way sharded frame; plus 8 rows run here
+  C5  3840x2160, 4096 spp, depth 50, 4100 spheres  4 full 3840-wide rows (digests) and 64 pixels
+                                                   on an 8x8 grid (oracle run in the test)
 Bar: bit-identical to the oracle on the subset (same accumulation chunk, read back through the
 ABI), per-channel RMS <= 1e-4 against the reference's sequential fp32 sum (north_star), and
 whole-frame properties (alpha 1, finite, radiance in [0, 1] for these scenes, segment counts
 between one and `depth` per sample). Reference loops: shader.comp:46-56, functions.glsl:73-91.
 """
+import hashlib
+import json
 import os
 
 import numpy as np
@@ -32,6 +39,30 @@ CONFIGS = {  # BASELINE.json configs, SURVEY.md 8(d)
     "c4": ("final", 1920, 1080, 1024, 10),
     "c5": ("stress4096", 3840, 2160, 4096, 50),
 }
+
+
+DIGESTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                       "full_frame_digests.json")
+
+
+def digests(name):
+    with open(DIGESTS) as f:
+        return json.load(f)[name]
+
+
+def row_digest(row):
+    return hashlib.sha256(np.ascontiguousarray(row, dtype="<f4").tobytes()).hexdigest()[:16]
+
+
+def check_digests(img, fx, what, rows=None):
+    """img [H][W][4] (or the fixture's rows) against the oracle's whole-frame digests: every
+    row's sha256 prefix (a failure names its rows), then the whole frame's sha256."""
+    sel = img if rows is None else img[rows]
+    bad = [i if rows is None else rows[i] for i, r in enumerate(sel)
+           if row_digest(r) != fx["row_sha256_16"][i]]
+    assert not bad, f"{what}: {len(bad)} rows differ from the oracle, first {bad[:10]}"
+    full = hashlib.sha256(np.ascontiguousarray(sel, dtype="<f4").tobytes()).hexdigest()
+    assert full == fx["frame_sha256"], what
 
 
 def bits(a):
@@ -81,6 +112,25 @@ def test_small_configs_whole_frame(oracle, name):
     assert st["segments"] == segs
     seq, _ = oracle.render(oracle.config(w, h, spp, depth), oracle.scene(scene))
     assert np.all(rms(got, seq) <= RMS_TOL)
+
+
+@pytest.mark.parametrize("name", ["c3", "c4"])
+def test_final_scene_configs_whole_frame_digest(name):
+    """Every pixel of the default C3 / C4 frame (the renderer's own quantum, vcrt_work_quantum = 4,
+    and scale 2^32) is bit-identical to the CPU oracle's render of the ENTIRE frame at full spp
+    and depth (functions.glsl:77-81's scan over shader.comp:42-57's whole dispatch), via the
+    committed digests; the segment total equals the oracle's; and the oracle's own whole-frame
+    per-channel RMS against the reference's sequential fp32 sum is within north_star's 1e-4."""
+    scene, w, h, spp, depth = CONFIGS[name]
+    fx = digests(name)
+    assert (fx["scene"], fx["width"], fx["height"], fx["spp"], fx["max_depth"], fx["rows"]) == \
+        (scene, w, h, spp, depth, None)
+    got, st = render_full(name)
+    assert st["accumulate_quantum"] == fx["quantum"]
+    assert st["accumulate_scale_log2"] == fx["scale_log2"] == 32
+    check_digests(got, fx, f"{name} whole frame")
+    assert st["segments"] == fx["segments"]
+    assert fx["finite"] and max(fx["rms_vs_sequential"]) <= RMS_TOL
 
 
 @pytest.mark.parametrize("name", ["c3", "c4"])
@@ -138,6 +188,9 @@ def test_c4_sharded_eight_ways_equals_one_gpu(oracle):
                 torch.cuda.synchronize()
     check_subset(frame.cpu().numpy(), full, "c4 8-way shards vs 1 GPU")
     assert segs == st1["segments"]
+    fx = digests("c4")  # and every pixel of the assembled frame against the oracle's
+    check_digests(frame.cpu().numpy(), fx, "c4 8-way assembled frame")
+    assert segs == fx["segments"]
 
 
 def read_pfm(path):
@@ -185,6 +238,20 @@ def test_cpp_host_api_reference_configuration_whole_frame(oracle, tmp_path, conf
     want, want_segs = oracle.render(oracle.config(w, h, spp, depth), oracle.scene("final"))
     check_subset(got, want[..., :3], f"vcrt_render {'configured' if configured else 'defaults'}")
     assert segs == {want_segs}
+
+
+def test_c5_full_rows_digest():
+    """Four full 3840-wide rows of the default C5 frame (sky, the sphere field, the ground) at
+    full spp (4096) and depth (50) with 4100 spheres, bit for bit against the oracle's digests
+    (tests/golden/full_frame_digests.json; the whole 4K frame is beyond the oracle: ~34 G
+    samples of a 4100-sphere linear scan)."""
+    scene, w, h, spp, depth = CONFIGS["c5"]
+    fx = digests("c5rows")
+    assert (fx["scene"], fx["width"], fx["height"], fx["spp"], fx["max_depth"]) == \
+        (scene, w, h, spp, depth)
+    got, st = render_full("c5")
+    assert st["accumulate_quantum"] == fx["quantum"]
+    check_digests(got, fx, "c5 rows", rows=fx["rows"])
 
 
 def test_c5_stress_pixel_grid(oracle):

@@ -242,3 +242,46 @@ def test_progressive_frame_blocks(oracle):
     c, _ = oracle.render(oracle.config(24, 16, 8, 6, chunk=3, frame_spp=4), scene)
     d, _ = oracle.render(oracle.config(24, 16, 8, 6, chunk=3), scene)
     assert np.abs(c.astype(np.float64) - d).max() < 1e-6
+
+
+def _full_frame_fixture():
+    with open(os.path.join(GOLDEN, "full_frame_digests.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name,rows", [("c3", [0, 540, 1079]), ("c4", [700])])
+def test_full_frame_digest_fixture(oracle, name, rows):
+    """tests/golden/full_frame_digests.json (the oracle over the whole C3 / C4 frames and four
+    full C5 rows, made by make_full_frame_digests.py) is reproduced by the oracle on sample rows:
+    the fixture's row digests are the oracle's own, at the renderer's default quantum. The GPU
+    tests (test_gpu_configs.py) assert every row of the GPU frames against the same digests."""
+    fx = _full_frame_fixture()
+    if name not in fx:
+        pytest.skip(f"{name} digests not generated yet")
+    fx = fx[name]
+    n = fx["height"] if fx["rows"] is None else len(fx["rows"])
+    assert len(fx["row_sha256_16"]) == n and fx["finite"]
+    assert max(fx["rms_vs_sequential"]) <= 1e-4  # north_star's per-channel bar, whole frame
+    cfg = oracle.config(fx["width"], fx["height"], fx["spp"], fx["max_depth"],
+                        quantum=fx["quantum"])
+    sc = oracle.scene(fx["scene"])
+    for i in rows:
+        y = fx["rows"][i] if fx["rows"] else i
+        img, _ = oracle.render(cfg, sc, rows=range(y, y + 1))
+        d = hashlib.sha256(np.ascontiguousarray(img[y], dtype="<f4").tobytes()).hexdigest()[:16]
+        assert d == fx["row_sha256_16"][i], (name, y)
+
+
+@pytest.mark.parametrize("name", ["c3", "c4", "c5rows"])
+def test_full_frame_digest_fixture_pixels(oracle, name):
+    """The fixture's eight sample pixels (float bits) re-rendered by the oracle: cheap enough for
+    C5's 4100-sphere, 4096-spp, depth-50 rows, whose full rows take minutes on the CPU."""
+    fx = _full_frame_fixture()
+    if name not in fx:
+        pytest.skip(f"{name} digests not generated yet")
+    fx = fx[name]
+    cfg = oracle.config(fx["width"], fx["height"], fx["spp"], fx["max_depth"],
+                        quantum=fx["quantum"])
+    px = fx["sample_pixels"]
+    got, _ = oracle.render_pixels(cfg, oracle.scene(fx["scene"]), [(p[0], p[1]) for p in px])
+    assert got.view(np.uint32).tolist() == [p[2:] for p in px]

@@ -111,6 +111,7 @@ class vcrt_stats(ctypes.Structure):
         ("accumulate_quantum", ctypes.c_int32),
         ("accumulate_scale_log2", ctypes.c_int32),
         ("cost_order", ctypes.c_int32),
+        ("scale_rerenders", ctypes.c_int32),
     ]
 
 
@@ -126,9 +127,7 @@ SIGNATURES = {
     "vcrt_work_chunk": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc)]),
     "vcrt_work_tail": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc),
                                         ctypes.POINTER(ctypes.c_int32)]),
-    "vcrt_work_scale": (ctypes.c_int32, [ctypes.POINTER(vcrt_render_desc),
-                                         ctypes.POINTER(vcrt_sphere), ctypes.c_int32,
-                                         ctypes.POINTER(ctypes.c_int32)]),
+    "vcrt_pixel_scale_log2": (ctypes.c_int32, [ctypes.c_float]),
     "vcrt_set_scene": (ctypes.c_int32, [ctypes.POINTER(vcrt_sphere), ctypes.c_int32]),
     "vcrt_draw_next_frame": (ctypes.c_int32, []),
     "vcrt_end": (ctypes.c_int32, []),

@@ -83,6 +83,7 @@ struct RendererState {
     uint32_t nch_magic[2] = {0u, 0u};  // TraceParams.nch_magic of the partition
     // deferred fetches (TraceParams.fetch_min / fetch_wait; VCRT_FETCH_MIN, VCRT_FETCH_WAIT)
     uint32_t fetch_min = 1u, fetch_wait = 0u;
+    int flat_block = 0;  // VCRT_FLAT_BLOCK: threads per group of the LDS flat scan (0: 256)
     uint32_t lds_per_cu = 0;     // LDS bytes per CU (160 KB on gfx950)
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
     int debug_stats = 0;  // 1: the stats kernels; 2: the product kernels with a debug buffer
@@ -95,7 +96,7 @@ struct RendererState {
     int32_t nspheres = 0;
     bool scene_bounded = false;  // every |center|, radius <= 2^30: discriminants stay finite
     bool radii_safe = false;     // every |radius| in [2^-40, 2^30] (kFlagRadiiSafe)
-    int32_t accum_log2 = vcrt::kAccumMaxScaleLog2;  // the scene's accumulation scale s
+    int32_t accum_log2 = vcrt::kAccumMaxScaleLog2;  // the scale s pixels start at (flags)
     float4* d_geom = nullptr;  // pair-SoA groups of four (+1 padding group)
     float4* d_center_radius = nullptr;
     float4* d_shade = nullptr;
@@ -123,6 +124,12 @@ struct RendererState {
     // d_accum holds zeros: a memset, or the last resolve wrote them back (vcrt_resolve
     // zero_accum), so a non-progressive frame needs no memset of its own
     bool accum_clean = false;
+    // Outlier quanta (vcrt_math.h "Accumulation"): [total_pixels] the float bits of each pixel's
+    // largest |quantum sum| that passed 2^12 (0: none); once one has, every frame of the
+    // configuration quantizes each pixel at its own scale (pixel_scale, kFlagPixelScale)
+    uint32_t* d_pixel_emax = nullptr;
+    bool pixel_scale = false;
+    int32_t min_scale = vcrt::kAccumMaxScaleLog2;  // the smallest pixel scale so far
     uint64_t accumulated = 0;               // samples per pixel accumulated (progressive)
     // the host's jitter (jx, jy) of a frame's sample indices: two pinned buffers used in turn,
     // each reused only once the copy recorded by its event is done (progressive frames set up
@@ -140,6 +147,11 @@ struct RendererState {
     float4* d_fb = nullptr;  // current render target (own or caller-provided)
     size_t fb_bytes = 0;
     void* d_counters = nullptr;
+    // the counters' first four u64 (outlier max, segments, work tallies), read back each frame:
+    // host-pinned, written by vcrt_resolve (which then zeroes d_counters: counters_clean) or
+    // copied when no resolve runs
+    unsigned long long* h_counters = nullptr;
+    bool counters_clean = false;
     uint32_t tiles_x = 0, local_tiles = 0;
     uint32_t local_elems = 0;   // float4 elements of the rank-local framebuffer
     uint64_t local_pixels = 0;  // frame pixels this rank renders
@@ -243,40 +255,6 @@ int32_t work_quantum(const vcrt_render_desc& d) {
     int32_t q = kDefaultQuantum;
     while ((d.samples_per_pixel + q - 1) / q > vcrt::kAccumMaxChunks) q *= 2;
     return q;
-}
-
-// The accumulation scale 2^s of a scene (vcrt_math.h "Accumulation"). One sample's radiance is
-// the sky's factor (<= 1) times the attenuations of its bounces: albedo * param for Lambertian
-// (textures.glsl:22), albedo for metal (:60), 1 for glass; so |radiance| <= R = A^depth, A the
-// largest per-bounce factor of the scene and at least 1 (the kernel's (int) of texture.x picks
-// the material; ids it cannot convert count as both). A quantum of G samples sums to at most
-// G R, and s is the largest integer <= 32 with G R 2^s < 2^44: every finite quantum sum then
-// quantizes below 2^44 and the pixel's exact sum stays below 2^53. The slack factors cover the
-// fp32 roundings (two per bounce, the sky's mix, the quantum's additions). Non-finite factors are
-// left out: they only make a sample's radiance non-finite, which makes its pixel NaN (its
-// quantum sum fails the 2^44 check). kAccumNoScale when R is beyond any scale (s < -80).
-constexpr int32_t kAccumNoScale = INT32_MIN;
-int32_t accum_scale_log2(const vcrt_sphere* sp, int32_t n, int32_t depth, int32_t quantum) {
-    double a = 1.0;
-    for (int32_t i = 0; i < n; i++) {
-        const float id = sp[i].texture[0];
-        const bool known = std::fabs(id) < 0x1p31f;  // (int) defined; NaN compares false
-        const int32_t t = known ? static_cast<int32_t>(id) : 0;
-        const bool lam = !known || t == VCRT_TEXTURE_LAMBERTIAN;
-        const bool met = !known || t == VCRT_TEXTURE_METAL;
-        for (int c = 0; c < 3; c++) {
-            const double col = std::fabs(static_cast<double>(sp[i].colour[c]));
-            const double f = col * std::fabs(static_cast<double>(sp[i].texture[1]));
-            if (lam && std::isfinite(f)) a = std::max(a, f);
-            if (met && std::isfinite(col)) a = std::max(a, col);
-        }
-    }
-    const double r = std::pow(a * (1.0 + 0x1p-22), std::max(depth, 1)) * (1.0 + 0x1p-20) *
-                     static_cast<double>(quantum) * (1.0 + static_cast<double>(quantum) * 0x1p-23);
-    if (!(r < 0x1p120)) return kAccumNoScale;
-    int32_t sc = vcrt::kAccumMaxScaleLog2;
-    while (sc > -80 && std::ldexp(r, sc) >= 0x1p44) --sc;
-    return std::ldexp(r, sc) < 0x1p44 ? sc : kAccumNoScale;
 }
 
 int32_t round_up(int32_t x, int32_t q) { return static_cast<int32_t>((int64_t{x} + q - 1) / q * q); }
@@ -589,6 +567,25 @@ VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Pa
     return VK_SUCCESS;
 }
 
+// Zero the pixels' sums and their outlier record (a new scene, vcrt_begin, a reset): every
+// pixel starts again at the scale 2^32 (vcrt_math.h "Accumulation").
+hipError_t reset_sums() {
+    if (g.d_accum) {
+        const hipError_t e = hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels));
+        if (e != hipSuccess) return e;
+        g.accum_clean = true;
+    }
+    if (g.d_pixel_emax) {
+        const hipError_t e =
+            hipMemset(g.d_pixel_emax, 0, sizeof(uint32_t) * static_cast<size_t>(g.total_pixels));
+        if (e != hipSuccess) return e;
+    }
+    g.pixel_scale = false;
+    g.min_scale = vcrt::kAccumMaxScaleLog2;
+    g.stats.accumulate_scale_log2 = vcrt::kAccumMaxScaleLog2;
+    return hipSuccess;
+}
+
 // TraceParams.jitter (vcrt_kernel_abi.h SetupJitterParams): the jitter term of the frame's
 // sample indices base .. base + spp - 1 (shader.comp:48), on the device with the tracer's own
 // operations.
@@ -796,6 +793,13 @@ KernelChoice select_kernel() {
         f = g.k_trace_cull_flat;
         fs = g.k_trace_cull_flat_stats;
         fname = "vcrt_trace_cull_flat";
+        // (experiments: a code object built with -DVCRT_FLAT_BLOCK=n launches n-thread groups)
+        int max_threads = 0;  // only a code object built for that size takes it
+        if (g.flat_block > 0 &&
+            hipFuncGetAttribute(&max_threads, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, f) ==
+                hipSuccess &&
+            max_threads >= g.flat_block)
+            block = static_cast<uint32_t>(g.flat_block);
         lds = tab_lds_flat + (block / 64) * vcrt::kWaveScratchBytes8;
     } else if (variant == VCRT_KERNEL_CULL_FLAT && flat_boxes) {
         f = g.k_trace_cull_flat_boxes;
@@ -872,19 +876,11 @@ int32_t vcrt_work_tail(const vcrt_render_desc* desc, int32_t* tail_chunk) {
     return work_tail(*desc, work_chunk(*desc), tail_chunk);
 }
 
-vcrt_result vcrt_work_scale(const vcrt_render_desc* desc, const vcrt_sphere* spheres,
-                            int32_t count, int32_t* scale_log2) {
-    if (!desc || !desc_valid(*desc) || !scale_log2 || count < 0 || (count > 0 && !spheres))
-        return VCRT_ERROR_INITIALIZATION_FAILED;
-    const int32_t q = work_quantum(*desc);
-    if (q >= desc->samples_per_pixel && !desc->progressive) {  // one quantum per pixel
-        *scale_log2 = vcrt::kAccumMaxScaleLog2;
-        return VCRT_SUCCESS;
-    }
-    const int32_t sc = accum_scale_log2(spheres, count, desc->max_depth, q);
-    if (sc == kAccumNoScale) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
-    *scale_log2 = sc;
-    return VCRT_SUCCESS;
+int32_t vcrt_pixel_scale_log2(float max_abs_quantum_sum) {
+    const float e = std::fabs(max_abs_quantum_sum);
+    uint32_t bits = 0;
+    std::memcpy(&bits, &e, sizeof(bits));
+    return vcrt::pixel_scale_log2(e >= 0x1p12f && std::isfinite(e) ? bits : 0u);
 }
 
 vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
@@ -1014,8 +1010,13 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         if ((r = to_vk(hipMalloc(&g.d_accum, bytes))) != VK_SUCCESS) return fail(r);
         if ((r = to_vk(hipMemset(g.d_accum, 0, bytes))) != VK_SUCCESS) return fail(r);
         g.accum_clean = true;
+        const size_t eb = sizeof(uint32_t) * static_cast<size_t>(g.total_pixels);
+        if ((r = to_vk(hipMalloc(&g.d_pixel_emax, eb))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemset(g.d_pixel_emax, 0, eb))) != VK_SUCCESS) return fail(r);
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
+    if ((r = to_vk(hipHostMalloc(&g.h_counters, 4 * sizeof(unsigned long long)))) != VK_SUCCESS)
+        return fail(r);
     if (const char* e = std::getenv("VCRT_DEBUG_STATS")) g.debug_stats = std::atoi(e);
     if (const char* e = std::getenv("VCRT_PRIMARY_LISTS")) g.primary_lists = std::atoi(e) != 0;
     if (const char* e = std::getenv("VCRT_CULL_LANE_TABLES"))
@@ -1038,6 +1039,10 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (const char* e = std::getenv("VCRT_ITEM_ORDER"))
         if (std::strcmp(e, "tile") == 0) g.work_flags &= ~vcrt::kFlagChunkMinor;
     if (const char* e = std::getenv("VCRT_STAGE_TABLES")) g.stage_tables = std::atoi(e) != 0;
+    if (const char* e = std::getenv("VCRT_FLAT_BLOCK")) {  // the LDS flat scan's group size
+        const int v = std::atoi(e) / 64 * 64;
+        g.flat_block = v <= 0 ? 0 : std::min(1024, v);
+    }
     if (const char* e = std::getenv("VCRT_FETCH_MIN"))
         g.fetch_min = static_cast<uint32_t>(std::max(1, std::atoi(e)));
     if (const char* e = std::getenv("VCRT_FETCH_WAIT"))
@@ -1071,11 +1076,6 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
 vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     if (count < 0 || (count > 0 && !spheres)) return VCRT_ERROR_INITIALIZATION_FAILED;
-    // the quantization scale of the quantum sums for this scene (one quantum per pixel: none)
-    const int32_t scale_log2 =
-        g.direct ? vcrt::kAccumMaxScaleLog2
-                 : accum_scale_log2(spheres, count, g.desc.max_depth, g.quantum);
-    if (scale_log2 == kAccumNoScale) return VCRT_ERROR_FORMAT_NOT_SUPPORTED;
     // Scan table: groups of four spheres in pair-SoA form
     //   (cx0,cx1,cy0,cy1) (cz0,cz1,r0²,r1²) (cx2,cx3,cy2,cy3) (cz2,cz3,r2²,r3²),
     // r² = radius*radius as hit_sphere computes it (functions.glsl:18). The last group is
@@ -1199,12 +1199,7 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     g.stats.nspheres = count;
     g.accumulated = 0;  // a new scene restarts progressive accumulation
     g.order_key = 0;    // and its cost order is measured again
-    if (g.d_accum) {
-        VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
-        g.accum_clean = true;
-    }
-    g.accum_log2 = scale_log2;
-    g.stats.accumulate_scale_log2 = scale_log2;
+    VCRT_TRY(reset_sums());
     g.scene_bounded = true;
     g.radii_safe = true;
     for (int32_t i = 0; i < count; i++) {
@@ -1255,7 +1250,11 @@ VkResult build_block_order(uint32_t total_blocks) {
     auto part = [&](uint32_t base, uint32_t nblocks, uint32_t nch, uint32_t samples) {
         for (uint32_t b = 0; b < nblocks; b++) {
             const uint32_t lt = b / nch, c = b - lt * nch;
-            const uint32_t s0 = (64u * c) / nch, s1 = std::min((64u * c + 63u) / nch, 63u);
+            // chunk-minor: slots (64 c) / nch .. (64 c + 63) / nch; tile-wide blocks
+            // (VCRT_ITEM_ORDER=tile): one chunk of all 64 slots
+            const bool cm = (g.work_flags & vcrt::kFlagChunkMinor) != 0u;
+            const uint32_t s0 = cm ? (64u * c) / nch : 0u;
+            const uint32_t s1 = cm ? std::min((64u * c + 63u) / nch, 63u) : 63u;
             uint64_t sum = 0;
             for (uint32_t sl = s0; sl <= s1; sl++) sum += cost[lt * 64u + sl];
             bc[base + b] = sum * samples * 64u / (s1 - s0 + 1u);
@@ -1280,6 +1279,324 @@ VkResult build_block_order(uint32_t total_blocks) {
     }
     VCRT_TRY(hipMemcpy(g.d_block_order, order.data(), total_blocks * sizeof(uint32_t),
                        hipMemcpyHostToDevice));
+    return VK_SUCCESS;
+}
+
+// One render of the frame's samples (the tracer kernel and, when the pixels sum quanta, the
+// resolve pass) on the render stream, waited for; *outlier_max receives the float bits of the
+// largest |quantum sum| that did not fit its pixel's scale (0: none; vcrt_math.h
+// "Accumulation").
+static VkResult trace_frame(uint64_t spp_total, uint32_t* outlier_max) {
+    const uint32_t pixels = g.total_pixels;
+    vcrt::TraceParams p{};
+    p.geom = g.d_geom;
+    p.center_radius = g.d_center_radius;
+    p.shade = g.d_shade;
+    p.material = g.d_material;
+    p.jitter = g.d_jitter;
+    p.corner = g.d_corner;
+    p.out = g.d_fb;
+    p.accum = g.d_accum;
+    p.work = reinterpret_cast<uint32_t*>(static_cast<char*>(g.d_counters) + 256);
+    p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
+    p.debug = static_cast<unsigned long long*>(g.d_debug);
+    p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);
+    p.cgroup = g.d_cgroup;
+    p.cbound = g.d_cbound;
+    p.cbound_nf = g.d_cbound_nf;
+    p.cnode = g.d_cnode;
+    p.cnode_nf = g.d_cnode_nf;
+    p.ctop = g.d_ctop;
+    p.prim_info = g.d_prim_info;
+    p.prim_ids = g.d_prim_ids;
+    p.cam_rec = g.d_cam_rec;
+    p.ncgroups = g.ncgroups;
+    p.nbig = g.ncbig;
+    for (int k = 0; k < 4; k++) p.box_margin[k] = g.cmargin[k];
+    p.nspheres = g.nspheres;
+    p.width = g.desc.width;
+    p.height = g.desc.height;
+    p.spp = g.desc.samples_per_pixel;
+    p.max_depth = g.desc.max_depth;
+    p.rank = g.desc.rank;
+    p.world = g.desc.world_size;
+    p.tiles_x = g.tiles_x;
+    p.local_tiles = g.local_tiles;
+    p.total_items = g.total_items;
+    p.chunk = g.chunk;
+    p.quantum_mask = static_cast<uint32_t>(g.quantum - 1);
+    p.nchunks = g.nchunks;
+    p.tail_start = g.tail_start;
+    p.tail_chunk = g.tail_chunk;
+    p.tail_nchunks = g.tail_nchunks;
+    p.blocks_head = g.local_tiles * static_cast<uint32_t>(g.nchunks);
+    p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
+              (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
+              (g.direct ? vcrt::kFlagDirect : 0u) |
+              (g.pixel_scale ? vcrt::kFlagPixelScale : 0u) |
+              (static_cast<uint32_t>(g.accum_log2 + vcrt::kFlagScaleBias)
+               << vcrt::kFlagScaleShift);
+    // outlier quanta (vcrt_math.h "Accumulation"); the kernel's quantizing retire writes them
+    p.pixel_emax = g.d_pixel_emax;
+    p.outlier_max = static_cast<uint32_t*>(g.d_counters);  // u32 at 0 (zeroed every launch)
+    if (!g.direct && (p.pixel_emax == nullptr || g.d_accum == nullptr))
+        return VK_ERROR_INITIALIZATION_FAILED;
+    p.spp_total = static_cast<float>(spp_total);
+    p.region = nullptr;
+    p.fetch_min = g.fetch_min;
+    p.fetch_wait = g.fetch_wait;
+    p.nch_magic[0] = g.nch_magic[0];
+    p.nch_magic[1] = g.nch_magic[1];
+    for (int j = 0; j < 13; j++) p.sin_c[j] = vcrt::kSinC[j];
+    const std::array<float, 12> cam = camera_array();
+    for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
+    const KernelChoice kc = select_kernel();
+    hipFunction_t f = g.debug_stats == 1 ? kc.stats : kc.f;
+    const uint32_t block = kc.block;
+    uint32_t lds = kc.lds;
+    // the linear SMEM scan of a small scene stages its shading and jitter tables in LDS
+    // (TraceParams.stage_*): C2 (4 spheres, 64 spp) is latency-bound on those reads
+    p.stage_spheres = 0u;
+    p.stage_spp = 0u;
+    if (kc.f == g.k_trace_smem && g.nspheres > 0 && g.stage_tables) {
+        // in 64 bits: 16 * spp wraps 32 bits for spp >= 2^28
+        const uint64_t bytes = 48ull * static_cast<uint64_t>(g.nspheres) +
+                               16ull * static_cast<uint64_t>(g.desc.samples_per_pixel);
+        if (bytes <= kStageMaxBytes) {
+            p.stage_spheres = static_cast<uint32_t>(g.nspheres);
+            p.stage_spp = static_cast<uint32_t>(g.desc.samples_per_pixel);
+            lds = static_cast<uint32_t>((bytes + 15u) & ~15ull);
+        }
+    }
+    const int variant = kc.variant;
+    // the stage names the entry point this draw dispatches (Shader.cpp:89 names "main")
+    g.stage.pName = kc.name;
+    std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s%s", kc.name,
+                  g.debug_stats == 1 ? "_stats" : "");
+    int per_cu = g.desc.blocks_per_cu;
+    if (per_cu <= 0) {
+        per_cu = 0;
+        if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, lds) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        if (g.max_blocks_per_cu > 0) per_cu = std::min(per_cu, g.max_blocks_per_cu);
+    }
+    // Cost order. When the frame gives each lane of the persistent grid few items, its end
+    // is set by the last expensive items to start (an item's segments run one per wave
+    // iteration: a glass pixel's 16-sample item at depth 8 is ~100 iterations), not by the
+    // work. Then the first frame of a configuration counts each pixel's segments
+    // (TraceParams.pixel_cost), and later frames hand out the blocks longest items first
+    // (TraceParams.block_order, build_block_order); such frames also run at most kDrainWavesPerSimd
+    // waves per SIMD, so that the waves holding the last items advance faster. Only the
+    // schedule changes: the image depends on the quantum alone. Automatic for the linear
+    // scans' frames with few items per lane (C2), and for the cost partition (default_chunk:
+    // the 4- and 8-way shards of C4, where the flat scans launch their cost-order builds).
+    // Elsewhere the flat scans' static bottom-up order is already roughly cost-ordered (sky
+    // last) and keeps neighbouring blocks together: the cost order on their own partitions
+    // measured slower (C4 -0.5%, C3 -1.1%, 8-way shards at K = 16 + 128 x 4 -4%;
+    // profiles/r05_ab_log.md).
+    const uint32_t total_blocks =
+        g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
+    const bool cost_mode =
+        g.debug_stats != 1 && total_blocks > 0 && kc.cost != nullptr &&
+        (g.cost_order == 1 ||
+         (g.cost_order < 0 &&
+          (g.cost_partition ||
+           (kc.cost == kc.f &&  // (the linear scans)
+            static_cast<uint64_t>(g.total_items) <
+                kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block))));
+    if (cost_mode && kc.cost != kc.f) {  // the flat scans' cost-order build
+        f = kc.cost;
+        std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s_cost", kc.name);
+    }
+    if (cost_mode && g.desc.blocks_per_cu <= 0 && g.max_blocks_per_cu <= 0)
+        per_cu = std::min(per_cu, std::max(1, static_cast<int>(kDrainWavesPerSimd * 4u * 64u /
+                                                               block)));
+    // The accumulation ring (tracer.hip RingEntry): the LDS the workgroups leave free at
+    // this occupancy, up to 63 entries of 32 B per wave, when the frame sums chunk sums
+    // (not one chunk per pixel), its blocks are chunk-minor and its pixel indices leave the
+    // top bits for the entry. The occupancy must not drop for it.
+    p.ring_off = 0u;
+    p.ring_n = 0u;
+    uint32_t lds_launch = lds;
+    if (g.accum_ring && !g.direct && (g.work_flags & vcrt::kFlagChunkMinor) != 0u &&
+        static_cast<uint64_t>(g.local_tiles) * 64u <= (uint64_t{1} << vcrt::kRingQBits) &&
+        g.lds_per_cu > 0 && g.desc.blocks_per_cu <= 0) {
+        const uint32_t waves = block / 64u;
+        const uint32_t off = (lds + 15u) & ~15u;
+        // usable LDS per CU: measured, five 256-thread workgroups of 32512 B ran four per
+        // CU (-11% at C4) while 32000 B ran five, although 5 x 32512 < 160 KiB and the
+        // occupancy query allows them: budget 160000 B per CU
+        const uint32_t per_wg = std::min<uint32_t>(g.lds_per_cu, 160000u) /
+                                static_cast<uint32_t>(per_cu);
+        uint32_t n = per_wg > off ? std::min<uint32_t>(g.ring_max,
+                                                        (per_wg - off) / (32u * waves))
+                                  : 0u;
+        for (; n >= 8u; n -= 4u) {
+            int occ = 0;
+            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &occ, f, block, off + 32u * n * waves) == hipSuccess &&
+                occ >= per_cu)
+                break;
+        }
+        if (n >= 8u) {
+            p.ring_off = off;
+            p.ring_n = n;
+            lds_launch = off + 32u * n * waves;
+        }
+    }
+    g.stats.ring_entries = static_cast<int32_t>(p.ring_n);
+    const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
+    const uint64_t key = cost_mode ? order_key_of(kc.f, grid, total_blocks) : 0;
+    bool measure = false;
+    p.pixel_cost = nullptr;
+    p.block_order = nullptr;
+    if (cost_mode && key == g.order_key) {
+        p.block_order = g.d_block_order;
+        p.flags &= ~vcrt::kFlagReverseOrder;  // the order is the whole hand-out sequence
+    } else if (cost_mode) {
+        if (pixels > g.cost_words) {
+            if (g.d_pixel_cost) (void)hipFree(g.d_pixel_cost);
+            g.d_pixel_cost = nullptr;
+            g.cost_words = 0;
+            VCRT_TRY(hipMalloc(&g.d_pixel_cost, pixels * sizeof(uint32_t)));
+            g.cost_words = pixels;
+        }
+        VCRT_TRY(hipMemsetAsync(g.d_pixel_cost, 0, pixels * sizeof(uint32_t), g.stream));
+        p.pixel_cost = g.d_pixel_cost;
+        measure = true;
+    }
+    g.stats.cost_order = p.block_order != nullptr ? 1 : 0;
+    if (!g.counters_clean) VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
+    g.counters_clean = false;  // until this frame's resolve has read and zeroed them
+    if (g.debug_stats == 1) {  // the stats kernels' region counters, one row per wave
+        const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
+        if (words > g.region_words) {
+            if (g.d_region) (void)hipFree(g.d_region);
+            g.d_region = nullptr;
+            g.region_words = 0;
+            VCRT_TRY(hipMalloc(&g.d_region, words * sizeof(uint32_t)));
+            g.region_words = words;
+        }
+        VCRT_TRY(hipMemsetAsync(g.d_region, 0, words * sizeof(uint32_t), g.stream));
+        p.region = g.d_region;
+    }
+    if (!g.direct && !g.desc.progressive && !g.accum_clean)  // every frame sums from zero
+        VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
+    if (!g.direct) g.accum_clean = false;  // until this frame's resolve zeroes it
+    if (g.debug_stats) {
+        unsigned long long init[128] = {0, 0, 0, 0, 0, ~0ull};
+        if (g.debug_stats == 2) init[9] = init[10] = ~0ull;  // wave times: minima
+        VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
+                                g.stream));
+    }
+    VCRT_TRY(hipEventRecord(g.ev_start, g.stream));
+    VkResult r = launch(f, grid, block, lds_launch, p);
+    if (r != VK_SUCCESS) return r;
+    VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
+    bool resolved = false;
+    if (!g.direct) {
+        vcrt::ResolveParams rp{g.d_accum,
+                               g.d_fb,
+                               std::ldexp(1.0, -g.accum_log2),
+                               static_cast<float>(spp_total),
+                               g.desc.width,
+                               g.desc.height,
+                               g.desc.rank,
+                               g.desc.world_size,
+                               g.tiles_x,
+                               g.local_tiles,
+                               g.desc.progressive ? 0u : 1u,
+                               g.pixel_scale ? g.d_pixel_emax : nullptr,
+                               static_cast<unsigned long long*>(g.d_counters),
+                               g.h_counters,
+                               static_cast<uint32_t>(kCounterBytes / 4)};
+        const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
+        r = launch(g.k_resolve, rgrid, 256, 0, rp);
+        if (r != VK_SUCCESS) return r;
+        resolved = true;
+        g.accum_clean = !g.desc.progressive;
+        VCRT_TRY(hipEventRecord(g.ev_resolve, g.stream));
+    }
+    if (!resolved)  // (one quantum per pixel: no resolve pass)
+        VCRT_TRY(hipMemcpyAsync(g.h_counters, g.d_counters, 4 * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, g.stream));
+    VCRT_TRY(hipStreamSynchronize(g.stream));
+    g.counters_clean = resolved;
+    const unsigned long long* counters = g.h_counters;
+    float ms = 0.f;
+    VCRT_TRY(hipEventElapsedTime(&ms, g.ev_start, g.ev_stop));
+    g.stats.kernel_ms = ms;
+    if (!g.direct) {
+        VCRT_TRY(hipEventElapsedTime(&ms, g.ev_stop, g.ev_resolve));
+        g.stats.resolve_ms = ms;
+    }
+    g.stats.segments = counters[1];
+    g.stats.group_tests = counters[2];
+    g.stats.bound_tests = counters[3];
+    if (measure) {
+        const VkResult ro = build_block_order(total_blocks);
+        if (ro != VK_SUCCESS) return ro;
+        g.order_key = key;
+    }
+    if (g.debug_stats)
+        VCRT_TRY(hipMemcpy(g.stats.debug, g.d_debug, sizeof(g.stats.debug),
+                           hipMemcpyDeviceToHost));
+    if (g.debug_stats == 1 && p.region) {  // region counters summed over the waves
+        const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
+        std::vector<uint32_t> rows(words);
+        VCRT_TRY(hipMemcpy(rows.data(), g.d_region, words * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost));
+        for (size_t w = 0; w < words / kRegionCount; w++)
+            for (uint32_t k = 0; k < kRegionCount; k++)
+                g.stats.debug[kRegionDebugBase + k] += rows[w * kRegionCount + k];
+    }
+    g.stats.grid_blocks = static_cast<int32_t>(grid);
+    g.stats.block_threads = static_cast<int32_t>(block);
+    g.stats.kernel_variant = variant;
+    g.stats.lds_bytes = lds;  // tables and stacks; the ring adds ring_entries x 32 B per wave
+    g.stats.tables_in_lds = kc.f == g.k_trace_cull_flat_boxes ? 2 :
+                            (kc.f == g.k_trace_cull_flat || kc.f == g.k_trace_cull_lane_lds ||
+                             kc.f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
+    *outlier_max = static_cast<uint32_t>(counters[0]);
+    return VK_SUCCESS;
+}
+
+// Outlier quanta (vcrt_math.h "Accumulation"): the render just done saw a quantum sum too large
+// for its pixel's scale (every pixel starts at 2^32: |S| >= 2^12). The kernel recorded each such
+// pixel's largest |S| in d_pixel_emax; from now on every frame of this configuration quantizes
+// each pixel at its own scale, and this frame is rendered again -- a progressive frame together
+// with every frame before it, from zero, since their sums were quantized at the old scales. The
+// image then depends on each pixel's own samples only (any rank, any schedule). A render at the
+// recorded scales sees no outliers (the same samples); a later progressive frame may raise a
+// pixel's maximum, and then the same happens again.
+static VkResult rerender_scaled(uint64_t spp_total, uint32_t outlier_max) {
+    const uint64_t spp = static_cast<uint64_t>(g.desc.samples_per_pixel);
+    for (int attempt = 0; outlier_max != 0u; attempt++) {
+        if (attempt == 4) return VK_ERROR_UNKNOWN;  // cannot happen: the maxima only grow
+        g.pixel_scale = true;
+        g.min_scale = std::min(g.min_scale, vcrt::pixel_scale_log2(outlier_max));
+        g.stats.accumulate_scale_log2 = g.min_scale;
+        g.stats.scale_rerenders += 1;
+        outlier_max = 0u;
+        if (!g.desc.progressive) {
+            VkResult r = trace_frame(spp_total, &outlier_max);
+            if (r != VK_SUCCESS) return r;
+            continue;
+        }
+        VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels),
+                                g.stream));
+        for (uint64_t f = 0; f * spp < spp_total; f++) {
+            VkResult r = setup_jitter(f * spp);
+            if (r == VK_SUCCESS) {
+                uint32_t o = 0u;
+                r = trace_frame((f + 1) * spp, &o);
+                outlier_max = std::max(outlier_max, o);
+            }
+            if (r != VK_SUCCESS) return r;
+        }
+    }
     return VK_SUCCESS;
 }
 
@@ -1314,262 +1631,11 @@ vcrt_result vcrt_draw_next_frame(void) {
         if (rj != VK_SUCCESS) return rj;
     }
     if (pixels != 0 && g.desc.max_depth > 0) {
-        vcrt::TraceParams p{};
-        p.geom = g.d_geom;
-        p.center_radius = g.d_center_radius;
-        p.shade = g.d_shade;
-        p.material = g.d_material;
-        p.jitter = g.d_jitter;
-        p.corner = g.d_corner;
-        p.out = g.d_fb;
-        p.accum = g.d_accum;
-        p.work = reinterpret_cast<uint32_t*>(static_cast<char*>(g.d_counters) + 256);
-        p.segments = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 8);
-        p.debug = static_cast<unsigned long long*>(g.d_debug);
-        p.work_done = reinterpret_cast<unsigned long long*>(static_cast<char*>(g.d_counters) + 16);
-        p.cgroup = g.d_cgroup;
-        p.cbound = g.d_cbound;
-        p.cbound_nf = g.d_cbound_nf;
-        p.cnode = g.d_cnode;
-        p.cnode_nf = g.d_cnode_nf;
-        p.ctop = g.d_ctop;
-        p.prim_info = g.d_prim_info;
-        p.prim_ids = g.d_prim_ids;
-        p.cam_rec = g.d_cam_rec;
-        p.ncgroups = g.ncgroups;
-        p.nbig = g.ncbig;
-        for (int k = 0; k < 4; k++) p.box_margin[k] = g.cmargin[k];
-        p.nspheres = g.nspheres;
-        p.width = g.desc.width;
-        p.height = g.desc.height;
-        p.spp = g.desc.samples_per_pixel;
-        p.max_depth = g.desc.max_depth;
-        p.rank = g.desc.rank;
-        p.world = g.desc.world_size;
-        p.tiles_x = g.tiles_x;
-        p.local_tiles = g.local_tiles;
-        p.total_items = g.total_items;
-        p.chunk = g.chunk;
-        p.quantum_mask = static_cast<uint32_t>(g.quantum - 1);
-        p.nchunks = g.nchunks;
-        p.tail_start = g.tail_start;
-        p.tail_chunk = g.tail_chunk;
-        p.tail_nchunks = g.tail_nchunks;
-        p.blocks_head = g.local_tiles * static_cast<uint32_t>(g.nchunks);
-        p.flags = g.work_flags | (g.scene_bounded ? vcrt::kFlagSceneBounded : 0u) |
-                  (g.radii_safe ? vcrt::kFlagRadiiSafe : 0u) |
-                  (g.direct ? vcrt::kFlagDirect : 0u) |
-                  (static_cast<uint32_t>(g.accum_log2 + vcrt::kFlagScaleBias)
-                   << vcrt::kFlagScaleShift);
-        p.spp_total = static_cast<float>(spp_total);
-        p.region = nullptr;
-        p.fetch_min = g.fetch_min;
-        p.fetch_wait = g.fetch_wait;
-        p.nch_magic[0] = g.nch_magic[0];
-        p.nch_magic[1] = g.nch_magic[1];
-        for (int j = 0; j < 13; j++) p.sin_c[j] = vcrt::kSinC[j];
-        const std::array<float, 12> cam = camera_array();
-        for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
-        const KernelChoice kc = select_kernel();
-        hipFunction_t f = g.debug_stats == 1 ? kc.stats : kc.f;
-        const uint32_t block = kc.block;
-        uint32_t lds = kc.lds;
-        // the linear SMEM scan of a small scene stages its shading and jitter tables in LDS
-        // (TraceParams.stage_*): C2 (4 spheres, 64 spp) is latency-bound on those reads
-        p.stage_spheres = 0u;
-        p.stage_spp = 0u;
-        if (kc.f == g.k_trace_smem && g.nspheres > 0 && g.stage_tables) {
-            // in 64 bits: 16 * spp wraps 32 bits for spp >= 2^28
-            const uint64_t bytes = 48ull * static_cast<uint64_t>(g.nspheres) +
-                                   16ull * static_cast<uint64_t>(g.desc.samples_per_pixel);
-            if (bytes <= kStageMaxBytes) {
-                p.stage_spheres = static_cast<uint32_t>(g.nspheres);
-                p.stage_spp = static_cast<uint32_t>(g.desc.samples_per_pixel);
-                lds = static_cast<uint32_t>((bytes + 15u) & ~15ull);
-            }
-        }
-        const int variant = kc.variant;
-        // the stage names the entry point this draw dispatches (Shader.cpp:89 names "main")
-        g.stage.pName = kc.name;
-        std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s%s", kc.name,
-                      g.debug_stats == 1 ? "_stats" : "");
-        int per_cu = g.desc.blocks_per_cu;
-        if (per_cu <= 0) {
-            per_cu = 0;
-            if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, block, lds) !=
-                    hipSuccess ||
-                per_cu <= 0)
-                per_cu = 1;
-            if (g.max_blocks_per_cu > 0) per_cu = std::min(per_cu, g.max_blocks_per_cu);
-        }
-        // Cost order. When the frame gives each lane of the persistent grid few items, its end
-        // is set by the last expensive items to start (an item's segments run one per wave
-        // iteration: a glass pixel's 16-sample item at depth 8 is ~100 iterations), not by the
-        // work. Then the first frame of a configuration counts each pixel's segments
-        // (TraceParams.pixel_cost), and later frames hand out the blocks longest items first
-        // (TraceParams.block_order, build_block_order); such frames also run at most kDrainWavesPerSimd
-        // waves per SIMD, so that the waves holding the last items advance faster. Only the
-        // schedule changes: the image depends on the quantum alone. Automatic for the linear
-        // scans' frames with few items per lane (C2), and for the cost partition (default_chunk:
-        // the 4- and 8-way shards of C4, where the flat scans launch their cost-order builds).
-        // Elsewhere the flat scans' static bottom-up order is already roughly cost-ordered (sky
-        // last) and keeps neighbouring blocks together: the cost order on their own partitions
-        // measured slower (C4 -0.5%, C3 -1.1%, 8-way shards at K = 16 + 128 x 4 -4%;
-        // profiles/r05_ab_log.md).
-        const uint32_t total_blocks =
-            g.local_tiles * static_cast<uint32_t>(g.nchunks + g.tail_nchunks);
-        const bool cost_mode =
-            g.debug_stats != 1 && total_blocks > 0 && kc.cost != nullptr &&
-            (g.cost_order == 1 ||
-             (g.cost_order < 0 &&
-              (g.cost_partition ||
-               (kc.cost == kc.f &&  // (the linear scans)
-                static_cast<uint64_t>(g.total_items) <
-                    kCostOrderItemsPerLane * static_cast<uint64_t>(per_cu) * g.num_cus * block))));
-        if (cost_mode && kc.cost != kc.f) {  // the flat scans' cost-order build
-            f = kc.cost;
-            std::snprintf(g.stats.kernel, sizeof(g.stats.kernel), "%s_cost", kc.name);
-        }
-        if (cost_mode && g.desc.blocks_per_cu <= 0 && g.max_blocks_per_cu <= 0)
-            per_cu = std::min(per_cu, std::max(1, static_cast<int>(kDrainWavesPerSimd * 4u * 64u /
-                                                                   block)));
-        // The accumulation ring (tracer.hip RingEntry): the LDS the workgroups leave free at
-        // this occupancy, up to 63 entries of 32 B per wave, when the frame sums chunk sums
-        // (not one chunk per pixel), its blocks are chunk-minor and its pixel indices leave the
-        // top bits for the entry. The occupancy must not drop for it.
-        p.ring_off = 0u;
-        p.ring_n = 0u;
-        uint32_t lds_launch = lds;
-        if (g.accum_ring && !g.direct && (g.work_flags & vcrt::kFlagChunkMinor) != 0u &&
-            static_cast<uint64_t>(g.local_tiles) * 64u <= (uint64_t{1} << vcrt::kRingQBits) &&
-            g.lds_per_cu > 0 && g.desc.blocks_per_cu <= 0) {
-            const uint32_t waves = block / 64u;
-            const uint32_t off = (lds + 15u) & ~15u;
-            // usable LDS per CU: measured, five 256-thread workgroups of 32512 B ran four per
-            // CU (-11% at C4) while 32000 B ran five, although 5 x 32512 < 160 KiB and the
-            // occupancy query allows them: budget 160000 B per CU
-            const uint32_t per_wg = std::min<uint32_t>(g.lds_per_cu, 160000u) /
-                                    static_cast<uint32_t>(per_cu);
-            uint32_t n = per_wg > off ? std::min<uint32_t>(g.ring_max,
-                                                            (per_wg - off) / (32u * waves))
-                                      : 0u;
-            for (; n >= 8u; n -= 4u) {
-                int occ = 0;
-                if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(
-                        &occ, f, block, off + 32u * n * waves) == hipSuccess &&
-                    occ >= per_cu)
-                    break;
-            }
-            if (n >= 8u) {
-                p.ring_off = off;
-                p.ring_n = n;
-                lds_launch = off + 32u * n * waves;
-            }
-        }
-        g.stats.ring_entries = static_cast<int32_t>(p.ring_n);
-        const uint32_t grid = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(g.num_cus);
-        const uint64_t key = cost_mode ? order_key_of(kc.f, grid, total_blocks) : 0;
-        bool measure = false;
-        p.pixel_cost = nullptr;
-        p.block_order = nullptr;
-        if (cost_mode && key == g.order_key) {
-            p.block_order = g.d_block_order;
-            p.flags &= ~vcrt::kFlagReverseOrder;  // the order is the whole hand-out sequence
-        } else if (cost_mode) {
-            if (pixels > g.cost_words) {
-                if (g.d_pixel_cost) (void)hipFree(g.d_pixel_cost);
-                g.d_pixel_cost = nullptr;
-                g.cost_words = 0;
-                VCRT_TRY(hipMalloc(&g.d_pixel_cost, pixels * sizeof(uint32_t)));
-                g.cost_words = pixels;
-            }
-            VCRT_TRY(hipMemsetAsync(g.d_pixel_cost, 0, pixels * sizeof(uint32_t), g.stream));
-            p.pixel_cost = g.d_pixel_cost;
-            measure = true;
-        }
-        g.stats.cost_order = p.block_order != nullptr ? 1 : 0;
-        VCRT_TRY(hipMemsetAsync(g.d_counters, 0, kCounterBytes, g.stream));
-        if (g.debug_stats == 1) {  // the stats kernels' region counters, one row per wave
-            const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
-            if (words > g.region_words) {
-                if (g.d_region) (void)hipFree(g.d_region);
-                g.d_region = nullptr;
-                g.region_words = 0;
-                VCRT_TRY(hipMalloc(&g.d_region, words * sizeof(uint32_t)));
-                g.region_words = words;
-            }
-            VCRT_TRY(hipMemsetAsync(g.d_region, 0, words * sizeof(uint32_t), g.stream));
-            p.region = g.d_region;
-        }
-        if (!g.direct && !g.desc.progressive && !g.accum_clean)  // every frame sums from zero
-            VCRT_TRY(hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(pixels), g.stream));
-        if (!g.direct) g.accum_clean = false;  // until this frame's resolve zeroes it
-        if (g.debug_stats) {
-            unsigned long long init[128] = {0, 0, 0, 0, 0, ~0ull};
-            if (g.debug_stats == 2) init[9] = init[10] = ~0ull;  // wave times: minima
-            VCRT_TRY(hipMemcpyAsync(g.d_debug, init, sizeof(init), hipMemcpyHostToDevice,
-                                    g.stream));
-        }
-        VCRT_TRY(hipEventRecord(g.ev_start, g.stream));
-        VkResult r = launch(f, grid, block, lds_launch, p);
+        g.stats.scale_rerenders = 0;
+        uint32_t outlier_max = 0u;
+        VkResult r = trace_frame(spp_total, &outlier_max);
+        if (r == VK_SUCCESS && outlier_max != 0u) r = rerender_scaled(spp_total, outlier_max);
         if (r != VK_SUCCESS) return r;
-        VCRT_TRY(hipEventRecord(g.ev_stop, g.stream));
-        if (!g.direct) {
-            vcrt::ResolveParams rp{g.d_accum,
-                                   g.d_fb,
-                                   std::ldexp(1.0, -g.accum_log2),
-                                   static_cast<float>(spp_total),
-                                   g.desc.width,
-                                   g.desc.height,
-                                   g.desc.rank,
-                                   g.desc.world_size,
-                                   g.tiles_x,
-                                   g.local_tiles,
-                                   g.desc.progressive ? 0u : 1u};
-            const uint32_t rgrid = std::min<uint32_t>((pixels + 255) / 256, 8192);
-            r = launch(g.k_resolve, rgrid, 256, 0, rp);
-            if (r != VK_SUCCESS) return r;
-            g.accum_clean = !g.desc.progressive;
-            VCRT_TRY(hipEventRecord(g.ev_resolve, g.stream));
-        }
-        unsigned long long counters[4] = {0, 0, 0, 0};
-        VCRT_TRY(hipMemcpyAsync(counters, g.d_counters, sizeof(counters), hipMemcpyDeviceToHost,
-                                g.stream));
-        VCRT_TRY(hipStreamSynchronize(g.stream));
-        float ms = 0.f;
-        VCRT_TRY(hipEventElapsedTime(&ms, g.ev_start, g.ev_stop));
-        g.stats.kernel_ms = ms;
-        if (!g.direct) {
-            VCRT_TRY(hipEventElapsedTime(&ms, g.ev_stop, g.ev_resolve));
-            g.stats.resolve_ms = ms;
-        }
-        g.stats.segments = counters[1];
-        g.stats.group_tests = counters[2];
-        g.stats.bound_tests = counters[3];
-        if (measure) {
-            const VkResult ro = build_block_order(total_blocks);
-            if (ro != VK_SUCCESS) return ro;
-            g.order_key = key;
-        }
-        if (g.debug_stats)
-            VCRT_TRY(hipMemcpy(g.stats.debug, g.d_debug, sizeof(g.stats.debug),
-                               hipMemcpyDeviceToHost));
-        if (g.debug_stats == 1 && p.region) {  // region counters summed over the waves
-            const size_t words = static_cast<size_t>(grid) * (block / 64u) * kRegionCount;
-            std::vector<uint32_t> rows(words);
-            VCRT_TRY(hipMemcpy(rows.data(), g.d_region, words * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost));
-            for (size_t w = 0; w < words / kRegionCount; w++)
-                for (uint32_t k = 0; k < kRegionCount; k++)
-                    g.stats.debug[kRegionDebugBase + k] += rows[w * kRegionCount + k];
-        }
-        g.stats.grid_blocks = static_cast<int32_t>(grid);
-        g.stats.block_threads = static_cast<int32_t>(block);
-        g.stats.kernel_variant = variant;
-        g.stats.lds_bytes = lds;  // tables and stacks; the ring adds ring_entries x 32 B per wave
-        g.stats.tables_in_lds = kc.f == g.k_trace_cull_flat_boxes ? 2 :
-                                (kc.f == g.k_trace_cull_flat || kc.f == g.k_trace_cull_lane_lds ||
-                                 kc.f == g.k_trace_cull_lane_lds_wide) ? 1 : 0;
     }
     if (g.comm && g.desc.world_size > 1) {
         // this rank's own render is complete (the stream synchronize above, no deadline); the
@@ -1608,6 +1674,7 @@ vcrt_result vcrt_end(void) {
     if (g.d_corner) (void)hipFree(g.d_corner);
     if (g.d_fb_own) (void)hipFree(g.d_fb_own);
     if (g.d_counters) (void)hipFree(g.d_counters);
+    if (g.h_counters) (void)hipHostFree(g.h_counters);
     if (g.d_debug) (void)hipFree(g.d_debug);
     if (g.d_region) (void)hipFree(g.d_region);
     if (g.d_pixel_cost) (void)hipFree(g.d_pixel_cost);
@@ -1617,6 +1684,7 @@ vcrt_result vcrt_end(void) {
     if (g.ev_stop) (void)hipEventDestroy(g.ev_stop);
     if (g.ev_resolve) (void)hipEventDestroy(g.ev_resolve);
     if (g.d_accum) (void)hipFree(g.d_accum);
+    if (g.d_pixel_emax) (void)hipFree(g.d_pixel_emax);
     if (g.d_srgb_thresholds) (void)hipFree(g.d_srgb_thresholds);
     if (g.d_srgb) (void)hipFree(g.d_srgb);
     comm_release(false);
@@ -1743,10 +1811,7 @@ vcrt_result vcrt_assemble_tiles(const void* gathered, void* frame, int32_t width
 vcrt_result vcrt_reset_accumulation(void) {
     if (!g.begun) return VCRT_ERROR_INITIALIZATION_FAILED;
     VCRT_TRY(hipStreamSynchronize(g.stream));
-    if (g.d_accum) {
-        VCRT_TRY(hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels)));
-        g.accum_clean = true;
-    }
+    VCRT_TRY(reset_sums());
     g.accumulated = 0;
     return setup_jitter(0);
 }

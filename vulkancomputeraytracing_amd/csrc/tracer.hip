@@ -1778,25 +1778,38 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
                 P.out[out_index] = make_float4(acc.x / P.spp_total, acc.y / P.spp_total,
                                                acc.z / P.spp_total, 1.0f);
             } else {
-                // the quantum sum, quantized: RN_even(S * 2^s) (an integer below 2^44: the
-                // scene's scale 2^s, from the flags word), summed exactly over the pixel's quanta in double;
-                // |S * 2^s| >= 2^44 (infinite or NaN radiance) makes the pixel NaN (vcrt_math.h
-                // "Accumulation"). (Three compares with |.| modifiers: NaN compares false; the
-                // NaN case in a real branch, so the common path converts without selects.)
-                // 2^s built from s + 128 in the flags' top byte (scalar ops, no load)
-                const float sc = __uint_as_float(
+                // the quantum sum, quantized: RN_even(S * 2^s) (an integer below 2^44), summed
+                // exactly over the pixel's quanta in double (vcrt_math.h "Accumulation"). The
+                // scale: 2^32 from s + 128 in the flags' top byte (scalar ops, no load), or with
+                // kFlagPixelScale the pixel's own from pixel_emax (a wave-uniform branch).
+                // (Three compares with |.| modifiers: NaN compares false; the rare cases in a
+                // real branch, so the common path converts without selects.)
+                float sc = __uint_as_float(
                     ((P.flags >> kFlagScaleShift) + (127u - (uint32_t)kFlagScaleBias)) << 23);
+                const uint32_t qi = q & kQMask, ent = q >> kRingQBits;
+                if ((P.flags & kFlagPixelScale) != 0u) {
+                    asm volatile("");
+                    sc = __uint_as_float((uint32_t)(pixel_scale_log2(P.pixel_emax[qi]) + 127) << 23);
+                }
                 float ax = acc.x * sc, ay = acc.y * sc, az = acc.z * sc;
                 if (!(fabsf(ax) < kAccumQLimit && fabsf(ay) < kAccumQLimit &&
                       fabsf(az) < kAccumQLimit)) {
                     asm volatile("");
                     region(rrow, reg::kRetireNan);
-                    ax = ay = az = __builtin_nanf("");
+                    if (__builtin_isfinite(acc.x) && __builtin_isfinite(acc.y) &&
+                        __builtin_isfinite(acc.z)) {
+                        // an outlier quantum: its pixel needs a smaller scale; the host renders
+                        // the frame again with pixel_emax (this frame's sums are discarded)
+                        const uint32_t mb = __float_as_uint(
+                            fmaxf(fabsf(acc.x), fmaxf(fabsf(acc.y), fabsf(acc.z))));
+                        atomicMax(P.pixel_emax + qi, mb);
+                        atomicMax(P.outlier_max, mb);
+                    }
+                    ax = ay = az = __builtin_nanf("");  // infinite or NaN radiance: a NaN pixel
                 }
                 const double v0 = (double)__builtin_rintf(ax);
                 const double v1 = (double)__builtin_rintf(ay);
                 const double v2 = (double)__builtin_rintf(az);
-                const uint32_t qi = q & kQMask, ent = q >> kRingQBits;
                 // the pixel's ring entry while it still holds this pixel (LDS atomics; a claim
                 // that takes the entry for another pixel clears the lane's entry field), else
                 // global memory (two branches: a pointer that may be either would make flat
@@ -2337,6 +2350,9 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
 
 }  // namespace
 
+#ifndef VCRT_FLAT_BLOCK
+#define VCRT_FLAT_BLOCK 256  // threads per workgroup the LDS flat scan is compiled for
+#endif
 #ifndef VCRT_FLAT_WAVES
 #define VCRT_FLAT_WAVES 5  // waves per SIMD the flat scans are compiled for (LDS allows 5)
 #endif
@@ -2379,7 +2395,7 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_cull_lane_lds_stats
 
 // Per-lane scan with the exact phase flattened over the wave (exact_flat): LDS tables plus
 // 3.5 KB of scratch per wave.
-extern "C" __global__ __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(VCRT_FLAT_BLOCK)
 __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, false, 4>(p, lds_tab);
@@ -2387,7 +2403,7 @@ __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat(
 
 // The flat scans' cost-order builds (vcrt_draw_next_frame "cost order"): the product kernel plus
 // the per-pixel segment count of the measuring frame and the block order of later frames.
-extern "C" __global__ __launch_bounds__(256)
+extern "C" __global__ __launch_bounds__(VCRT_FLAT_BLOCK)
 __attribute__((amdgpu_waves_per_eu(VCRT_FLAT_WAVES))) void vcrt_trace_cull_flat_cost(TraceParams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
     trace_impl<false, false, 4, true>(p, lds_tab);
@@ -2477,14 +2493,25 @@ extern "C" __global__ __launch_bounds__(256) void vcrt_trace_smem_stats(TracePar
 
 // Exact sample sums -> pixels (vcrt_math.h "Accumulation"; shader.comp:56 divides by SPP).
 extern "C" __global__ __launch_bounds__(256) void vcrt_resolve(ResolveParams p) {
+    if (p.counters != nullptr && blockIdx.x == 0u) {  // the tracer's counters: read, then zeroed
+        unsigned long long v = 0ull;
+        if (threadIdx.x < 4u) v = p.counters[threadIdx.x];
+        __syncthreads();
+        if (threadIdx.x < 4u) p.counters_out[threadIdx.x] = v;
+        uint32_t* w = reinterpret_cast<uint32_t*>(p.counters);
+        for (uint32_t i = threadIdx.x; i < p.counter_words; i += blockDim.x) w[i] = 0u;
+        __threadfence_system();
+    }
     const uint32_t elems = p.local_tiles * 64u;
-    const double st = (double)p.spp_total, inv = p.inv_scale;
+    const double st = (double)p.spp_total, inv_all = p.inv_scale;
     for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < elems;
          q += gridDim.x * blockDim.x) {
         const Pixel px = pixel_of(q, (uint32_t)p.width, (uint32_t)p.height, p.tiles_x,
                                   (uint32_t)p.world, (uint32_t)p.rank);
         if (!px.valid) continue;
         const double4 s = *reinterpret_cast<const double4*>(p.accum + 4u * q);
+        const double inv = p.pixel_emax ? __builtin_ldexp(1.0, -pixel_scale_log2(p.pixel_emax[q]))
+                                        : inv_all;
         if (p.zero_accum) *reinterpret_cast<double4*>(p.accum + 4u * q) = double4{0.0, 0.0, 0.0, 0.0};
         p.out[px.out_index] = make_float4(resolve_channel(s.x, inv, st),
                                           resolve_channel(s.y, inv, st),

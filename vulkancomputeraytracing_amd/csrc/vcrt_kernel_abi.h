@@ -119,6 +119,12 @@ struct TraceParams {
     // block a part hands out to the block of that part to run (the reverse flag is then off)
     uint32_t* pixel_cost;
     const uint32_t* block_order;
+    // Outlier quanta (vcrt_math.h "Accumulation"): a quantum sum with |S * 2^s| >= 2^44 (finite)
+    // atomicMax-es the float bits of its largest |channel| into pixel_emax[local pixel] and into
+    // *outlier_max; with kFlagPixelScale every pixel quantizes at pixel_scale_log2(pixel_emax[.])
+    // instead of the flags' scale
+    uint32_t* pixel_emax;
+    uint32_t* outlier_max;
 };
 
 constexpr uint32_t kQueueStride = 32;  // u32s between the work-queue counters (128 B)
@@ -149,6 +155,7 @@ constexpr uint32_t kFlagRadiiSafe = 16u;  // every |radius| in [2^-40, 2^30] (ho
                                          // shading's (p - c) / r may take the unscaled division
 constexpr uint32_t kFlagScaleShift = 24u;  // TraceParams.flags: s + kFlagScaleBias
 constexpr int32_t kFlagScaleBias = 128;
+constexpr uint32_t kFlagPixelScale = 32u;  // per-pixel scales from TraceParams.pixel_emax
 constexpr uint32_t kFlagDirect = 4u;  // one work item per pixel and frame, not progressive: the
                                       // lane writes the pixel itself (no sums, no resolve pass)
 
@@ -172,6 +179,13 @@ struct ResolveParams {
     int32_t width, height, rank, world;
     uint32_t tiles_x, local_tiles;
     uint32_t zero_accum;  // 1: write zeros back (the next frame sums from zero: no memset)
+    const uint32_t* pixel_emax;  // non-null: each pixel's own scale (vcrt_math.h pixel_scale_log2)
+    // the tracer's counters (TraceParams outlier_max, segments, work_done, work queues), or
+    // null: block 0 copies their first four u64 to counters_out (host-pinned) and then zeroes
+    // counter_words u32 of them, so the next frame needs neither a memset nor a read-back copy
+    unsigned long long* counters;
+    unsigned long long* counters_out;
+    uint32_t counter_words;
 };
 
 struct AssembleParams {

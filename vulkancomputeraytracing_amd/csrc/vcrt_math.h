@@ -437,16 +437,25 @@ VCRT_HD float schlick_r0(float cosine, float r0) {
 //     out = (float)((sum * 2^-s) / (double)spp_total).
 // Exact sums do not depend on the order of the additions, so the image depends on G and s
 // alone: not on the work items, the schedule or the number of GPUs (a sharded frame equals the
-// one-GPU frame bit for bit). The scale 2^s is per scene (accum_scale_log2): the largest s <= 32
-// with G * R * 2^s < 2^44, R a bound on one sample's radiance (the largest per-bounce
-// attenuation of the scene, at least 1, raised to MAX_RECURSION_LEVEL), so every finite quantum
-// sum fits; the reference scenes (R ~ 1) take s = 32, which keeps every S >= 2^-9 exactly. The
-// quantized combination differs from the fp32 sequential sum by less than that sum's own
-// rounding error. A quantum sum with |S * 2^s| >= 2^44 -- only infinite or
-// NaN radiance reaches it -- makes the pixel NaN.
+// one-GPU frame bit for bit). The scale 2^s is per pixel (pixel_scale_log2), from E, the
+// largest |S| of the pixel's finite quantum sums (every channel, every progressive frame so
+// far): s = 32 while E < 2^12 -- every pixel of the reference scenes, whose radiance is <= 1 per
+// sample, which keeps every S >= 2^-9 exactly -- else the largest s with E * 2^s < 2^44. A pixel
+// depends on its own samples only, so any rank computes its scale alone. The kernel quantizes at
+// the scale it was given (32, or the pixel's from TraceParams.pixel_emax); a quantum with
+// |S * 2^s| >= 2^44 records max|S| there (atomicMax on the float bits) and the host renders the
+// frame again with every pixel at its own scale (capi.cpp "Outlier quanta"). A NaN or infinite
+// quantum sum makes the pixel NaN. The quantized combination differs from the fp32 sequential
+// sum by less than that sum's own rounding error.
 constexpr int32_t kAccumMaxScaleLog2 = 32;
 constexpr float kAccumQLimit = 0x1p44f;   // |q| bound of one quantum sum
 constexpr int32_t kAccumMaxChunks = 512;  // quanta per pixel (progressive frames included)
+
+// The scale s of a pixel whose largest finite |quantum sum| has the float bits emax_bits (0: none
+// reached 2^12): 32, or 43 - floor(log2 E) = 170 - biased exponent (E >= 2^12 is normal).
+VCRT_HD int32_t pixel_scale_log2(uint32_t emax_bits) {
+    return emax_bits == 0u ? kAccumMaxScaleLog2 : 170 - static_cast<int32_t>(emax_bits >> 23);
+}
 
 // One channel of a pixel from the exact sum of its quantized quantum sums; inv_scale = 2^-s.
 VCRT_HD float resolve_channel(double s, double inv_scale, double spp_total) {

@@ -88,16 +88,11 @@ def work_tail(desc: RenderDesc) -> tuple[int, int]:
     return (t, kt.value) if t > 0 else (0, 0)
 
 
-def work_scale(desc: RenderDesc, scene="final") -> int:
-    """s of the quantization scale 2^s of the quantum sums the renderer uses for `desc` and a
-    scene (vcrt_work_scale: host only, no GPU): the oracle restates the same rule."""
-    arr = builtin_scene(scene) if isinstance(scene, (str, int)) else scene
-    arr = np.ascontiguousarray(arr, dtype=SPHERE_DTYPE)
-    s = ctypes.c_int32(0)
-    N.check("vcrt_work_scale", N.lib().vcrt_work_scale(
-        ctypes.byref(desc.to_c()), arr.ctypes.data_as(ctypes.POINTER(N.vcrt_sphere)), len(arr),
-        ctypes.byref(s)))
-    return s.value
+def pixel_scale_log2(max_abs_quantum_sum: float) -> int:
+    """s of a pixel's quantization scale 2^s from its largest |quantum sum| (vcrt_pixel_scale_log2:
+    host only, no GPU): 32 below 2^12, else the largest s with max * 2^s < 2^44. The oracle
+    restates the same rule (oracle_pixel_scale_log2)."""
+    return N.lib().vcrt_pixel_scale_log2(float(max_abs_quantum_sum))
 
 
 def tiles_for_rank(width: int, height: int, world: int, rank: int) -> list[int]:
