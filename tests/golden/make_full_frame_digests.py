@@ -32,8 +32,8 @@ OUT = os.path.join(ROOT, "tests", "golden", "full_frame_digests.json")
 CONFIGS = {  # name: (scene, W, H, spp, depth, quantum, rows or None for the whole frame)
     "c3": ("final", 1920, 1080, 256, 10, 4, None),
     "c4": ("final", 1920, 1080, 1024, 10, 4, None),
-    # C5: four full 3840-wide rows at full spp (4096) and depth (50): sky, sphere field, ground
-    "c5rows": ("stress4096", 3840, 2160, 4096, 50, 8, [400, 1000, 1300, 1900]),
+    # C5: eight full 3840-wide rows at full spp (4096) and depth (50): sky, sphere field, ground
+    "c5rows": ("stress4096", 3840, 2160, 4096, 50, 8, [120, 400, 700, 1000, 1300, 1600, 1900, 2150]),
 }
 
 

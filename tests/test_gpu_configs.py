@@ -12,7 +12,7 @@ spp and depth:
                                                    build container); plus 8 rows run here
   C4  1920x1080, 1024 spp, depth 10, final scene   the same whole-frame digests, also for the
                                                    8-way sharded frame; plus 8 rows run here
-  C5  3840x2160, 4096 spp, depth 50, 4100 spheres  4 full 3840-wide rows (digests) and 64 pixels
+  C5  3840x2160, 4096 spp, depth 50, 4100 spheres  8 full 3840-wide rows (digests) and 64 pixels
                                                    on an 8x8 grid (oracle run in the test)
 Bar: bit-identical to the oracle on the subset (same accumulation chunk, read back through the
 ABI), per-channel RMS <= 1e-4 against the reference's sequential fp32 sum (north_star), and
@@ -241,7 +241,7 @@ def test_cpp_host_api_reference_configuration_whole_frame(oracle, tmp_path, conf
 
 
 def test_c5_full_rows_digest():
-    """Four full 3840-wide rows of the default C5 frame (sky, the sphere field, the ground) at
+    """Eight full 3840-wide rows of the default C5 frame (sky, the sphere field, the ground) at
     full spp (4096) and depth (50) with 4100 spheres, bit for bit against the oracle's digests
     (tests/golden/full_frame_digests.json; the whole 4K frame is beyond the oracle: ~34 G
     samples of a 4100-sphere linear scan)."""

@@ -251,7 +251,7 @@ def _full_frame_fixture():
 
 @pytest.mark.parametrize("name,rows", [("c3", [0, 540, 1079]), ("c4", [700])])
 def test_full_frame_digest_fixture(oracle, name, rows):
-    """tests/golden/full_frame_digests.json (the oracle over the whole C3 / C4 frames and four
+    """tests/golden/full_frame_digests.json (the oracle over the whole C3 / C4 frames and eight
     full C5 rows, made by make_full_frame_digests.py) is reproduced by the oracle on sample rows:
     the fixture's row digests are the oracle's own, at the renderer's default quantum. The GPU
     tests (test_gpu_configs.py) assert every row of the GPU frames against the same digests."""

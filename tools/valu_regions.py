@@ -87,22 +87,14 @@ def is_salu(mn):
     return mn.startswith("s_") and not mn.startswith(_NOT_SALU)
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--hsaco", default=None)
-    p.add_argument("--product", default=os.path.join(ROOT, "vulkancomputeraytracing_amd", "lib",
-                                                     "vcrt_tracer.hsaco"))
-    p.add_argument("--kernel", default="vcrt_trace_cull_flat")
-    p.add_argument("--stats", required=True, help="stats-build render_once JSON (one frame)")
-    p.add_argument("--sq-valu", type=float, required=True,
-                   help="SQ_INSTS_VALU of the product frame (instructions, per dispatch)")
-    p.add_argument("--json", default=None)
-    p.add_argument("--kind", choices=("valu", "salu"), default="valu",
-                   help="salu: scalar ALU and branch instructions (s_* but memory, waits, "
-                        "nops), against SQ_INSTS_SALU given as --sq-valu")
-    p.add_argument("--detail", action="append", default=[],
-                   help="region name: also list its static VALU per innermost source line")
-    a = p.parse_args()
+def assign_regions(hsaco, product, kernel):
+    """Every instruction of `kernel` in the product code object with the region that holds it:
+    ([(address, mnemonic, operands, region)], label(region) -> name). hsaco: the
+    -gline-tables-only build (None: built by tools/mkab.sh lt)."""
+    class A:
+        pass
+    a = A()
+    a.hsaco, a.product, a.kernel = hsaco, product, kernel
     if a.hsaco is None:
         a.hsaco = subprocess.run(["bash", os.path.join(ROOT, "tools", "mkab.sh"), "lt"],
                                  env=dict(os.environ, EXTRA="-gline-tables-only"),
@@ -189,11 +181,41 @@ def main():
             return ev["kIter"]
         return -1  # prologue / epilogue: once per wave
 
+
+    def label(r):
+        if r < 0:
+            return "prologue/epilogue"
+        if r in names:
+            return names[r]
+        if ev["kShadeBase1"] <= r < ev["kShadeBase1"] + 16:
+            return "shade(sky after scan)." + sh_names.get(r - ev["kShadeBase1"], "?")
+        if ev["kShadeBase0"] <= r < ev["kShadeBase0"] + 16:
+            return "shade(camera phase)." + sh_names.get(r - ev["kShadeBase0"], "?")
+        return str(r)
+    return [(ad, mn, ops, region_of(chains[ad])) for ad, mn, ops in insts], label, chains
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--hsaco", default=None)
+    p.add_argument("--product", default=os.path.join(ROOT, "vulkancomputeraytracing_amd", "lib",
+                                                     "vcrt_tracer.hsaco"))
+    p.add_argument("--kernel", default="vcrt_trace_cull_flat")
+    p.add_argument("--stats", required=True, help="stats-build render_once JSON (one frame)")
+    p.add_argument("--sq-valu", type=float, required=True,
+                   help="SQ_INSTS_VALU of the product frame (instructions, per dispatch)")
+    p.add_argument("--json", default=None)
+    p.add_argument("--kind", choices=("valu", "salu"), default="valu",
+                   help="salu: scalar ALU and branch instructions (s_* but memory, waits, "
+                        "nops), against SQ_INSTS_SALU given as --sq-valu")
+    p.add_argument("--detail", action="append", default=[],
+                   help="region name: also list its static VALU per innermost source line")
+    a = p.parse_args()
+    insts_r, label, chains = assign_regions(a.hsaco, a.product, a.kernel)
     static = collections.Counter()
     where = collections.defaultdict(collections.Counter)
-    for ad, mn, _ in insts:
+    for ad, mn, _, r in insts_r:
         if (V.is_valu(mn) if a.kind == "valu" else is_salu(mn)):
-            r = region_of(chains[ad])
             static[r] += 1
             f, fl, ln = chains[ad][0]
             where[r][(fl, ln, f.split("(")[0][:40])] += 1
@@ -210,16 +232,6 @@ def main():
         rows.append((dyn, r, n, cnt))
     rows.sort(reverse=True)
 
-    def label(r):
-        if r < 0:
-            return "prologue/epilogue"
-        if r in names:
-            return names[r]
-        if ev["kShadeBase1"] <= r < ev["kShadeBase1"] + 16:
-            return "shade(sky after scan)." + sh_names.get(r - ev["kShadeBase1"], "?")
-        if ev["kShadeBase0"] <= r < ev["kShadeBase0"] + 16:
-            return "shade(camera phase)." + sh_names.get(r - ev["kShadeBase0"], "?")
-        return str(r)
     print(f"stats frame: {st['segments']} segments, {waves} waves, {d[0]} wave-iterations")
     K = a.kind.upper()
     print(f"{'dynamic ' + K:>14} {'share':>6} {'static':>6} {'entries':>12}  region")
