@@ -3,17 +3,16 @@ attribution (tools/valu_regions.py: every instruction of the product code object
 region x the region's entries in a stats frame of the same workload) weighted by the issue cost
 of each instruction's class, measured by tools/microbench_classes.hip on the same GPU.
 
-Per class two costs, both relative to v_mul_f32 (one quad-cycle of a SIMD's VALU per wave
-instruction):
-  pipe   -- the SIMD's VALU throughput cost (8 waves per SIMD, independent chains), and the
-            counter's own weighting SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU of the form (PMC run);
-  issue  -- one wave's issue interval (1 wave per SIMD), i.e. what the form costs the wave's own
-            instruction stream (SALU included: a scalar instruction takes the wave's issue slot).
-The weighted sums are compared with the product frame's SQ_ACTIVE_INST_VALU (+ the SALU issue,
-SQ_INSTS_SALU) and with the SIMDs' quad-cycles in the frame (1024 SIMDs x GRBM_GUI_ACTIVE / 4 ...).
+Costs are SIMD cycles per wave64 instruction, from GRBM_GUI_ACTIVE of the microbenchmark's
+dispatches (clock-independent), at 5 waves per SIMD (the flat kernel's occupancy; 8 independent
+chains per wave) and at 1 wave per SIMD (one wave's own issue interval). gfx950 measured three
+VALU rates: "fast" (v_add/sub/mul_f32, v_mov_b32, v_and/or/xor_b32, v_add_u32 with vector or
+literal operands: ~2.7 cycles), "normal" (everything else: fma, min/max, compares, selects,
+packed, f64, shifts, lane ops, and a fast op with a scalar operand: ~4.5 cycles) and
+transcendental (v_sqrt/v_rcp_f32 ~8.5, v_rcp_f64 ~16.6); scalar instructions ~4.6 per SIMD.
 
-  python tools/cycle_attrib.py --stats STATS.json --micro MICRO.json [--micro-pmc CSV]
-                               [--pmc PMC.json] [--out profiles/r06_cycle_attrib.txt]
+  python tools/cycle_attrib.py --stats STATS.json --micro-grbm GRBM.csv [--pmc PMC.json]
+                               [--out profiles/r06_cycle_attrib.txt]
 """
 import argparse
 import collections
@@ -29,85 +28,80 @@ import valu_regions as R  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CLASSES = [  # (class, pattern on the full mnemonic, encoding suffix included), first match wins
-    ("dpp", r".*_dpp$"),
-    ("sdwa", r".*_sdwa$"),
-    ("packed", r"^v_pk_"),
-    ("trans64", r"^v_(rcp|sqrt|rsq)_f64"),
-    ("trans", r"^v_(sqrt|rcp|rsq|rcp_iflag|exp|log|sin|cos)_f32"),
-    ("div", r"^v_div_(scale|fmas|fixup)_f(32|64)"),
-    ("cvt64", r"^v_cvt_.*f64|^v_cvt_f64"),
-    ("f64", r"^v_.*_f64"),
-    ("mul32", r"^v_(mul_lo_u32|mul_hi_u32|mul_hi_i32|mad_u64_u32|mad_i64_i32|mul_lo_i32)"),
-    ("int64", r"^v_(lshl_add_u64|lshlrev_b64|lshrrev_b64|ashrrev_i64|mov_b64)"),
-    ("lane", r"^v_(readlane|readfirstlane|writelane)_b32"),
-    ("cndmask_vcc", r"^v_cndmask_b32_e32$"),
-    ("cndmask_sgpr", r"^v_cndmask_b32_e64$"),
-    ("cmp", r"^v_cmpx?_"),
-    ("vop2", r"^v_.*_e32$"),   # VOP1 / VOP2 encodings (4-byte, no modifiers)
-    ("vop3", r"^v_"),          # VOP3 encodings (8-byte: _e64 and VOP3-only forms)
-]
-# the microbenchmark form that stands for each class
-FORM = {"vop2": "v_mul_f32", "vop3": "v_fma_f32", "cmp": "v_cmp_lt_f32",
-        "cndmask_vcc": "v_cndmask_b32", "cndmask_sgpr": "v_cndmask_b32_e64_sgpr",
-        "packed": "v_pk_fma_f32", "f64": "v_fma_f64", "cvt64": "v_cvt_f64_f32",
-        "trans": "v_sqrt_f32", "trans64": "v_rcp_f64", "div": "v_div_scale_f32",
-        "mul32": "v_mul_lo_u32", "int64": "v_lshl_add_u64", "lane": "v_readfirstlane_b32",
-        "dpp": "v_add_u32_dpp", "sdwa": "v_fma_f32", "salu": "s_add_u32"}
+# double-rate VALU operations on gfx950 (microbench_classes: ~2.7 cycles per wave64 instruction at
+# 5 waves per SIMD against ~4.5), when no operand is a scalar register
+FAST = {"v_add_f32", "v_sub_f32", "v_subrev_f32", "v_mul_f32", "v_mov_b32", "v_and_b32",
+        "v_or_b32", "v_xor_b32", "v_add_u32", "v_sub_u32", "v_subrev_u32"}
+TRANS = re.compile(r"^v_(sqrt|rcp|rsq|rcp_iflag|exp|log|sin|cos)_f32")
+TRANS64 = re.compile(r"^v_(rcp|sqrt|rsq)_f64")
+SCALAR_OPERAND = re.compile(r"(^|[\s,\[-])(s\d+|s\[\d+:\d+\]|vcc(_lo|_hi)?|exec(_lo|_hi)?|m0|ttmp)")
+# the microbenchmark kernel whose cycles stand for each class
+KERNEL = {"fast": "k_mul", "normal": "k_fma", "trans": "k_sqrt", "trans64": "k_rcp64",
+          "salu": "k_salu"}
+# sub-labels of the normal class, for the report
+SUBCLASS = [("packed", r"^v_pk_"), ("f64", r"_f64"), ("cmp", r"^v_cmpx?_"),
+            ("cndmask", r"^v_cndmask"), ("minmax", r"^v_(max|min|med)"),
+            ("fma", r"^v_(fma|fmac|mad)"), ("lane", r"^v_(readlane|readfirstlane|writelane)"),
+            ("dpp", r"_dpp$"), ("div", r"^v_div_"), ("int", r"^v_")]
 
 
-def klass(mn):
+def base(mn):
+    return re.sub(r"_e(32|64)$", "", mn)
+
+
+def klass(mn, ops):
+    """(class, sub-label) of one instruction, or None if it is neither VALU nor SALU."""
     if R.is_salu(mn):
-        return "salu"
+        return "salu", "salu"
     if not V.is_valu(mn):
         return None
-    for c, pat in CLASSES:
-        if re.match(pat, mn):
-            return c
-    return None
+    b = base(mn)
+    if TRANS64.match(b):
+        return "trans64", "trans64"
+    if TRANS.match(b):
+        return "trans", "trans"
+    operands = ops.split(" ", 1)[1] if " " in ops.strip() else ""
+    if b in FAST and not SCALAR_OPERAND.search(operands):
+        return "fast", "fast"
+    if b in FAST:
+        return "normal", "fast op, scalar operand"
+    for lab, pat in SUBCLASS:
+        if re.search(pat, b):
+            return "normal", lab
+    return "normal", "other"
 
 
-def micro_costs(micro, micro_pmc):
-    forms = {f["form"]: f for f in micro["forms"]}
-    ref = forms["v_mul_f32"]
+def grbm_costs(path):
+    """Cycles per wave64 instruction per microbenchmark kernel at 1 / 5 / 8 waves per SIMD: each
+    kernel ran 3 configurations (1, 8, 5 waves per SIMD) x (1 warm-up + 5 timed) dispatches."""
+    per = collections.defaultdict(dict)
+    for row in csv.DictReader(open(path)):
+        d = int(row["Dispatch_Id"])
+        per[d]["k"] = row["Kernel_Name"].split("(")[0].strip()
+        if row["Counter_Name"] == "GRBM_GUI_ACTIVE":
+            per[d]["g"] = per[d].get("g", 0.0) + float(row["Counter_Value"])
+    byk = collections.defaultdict(list)
+    for d in sorted(per):
+        byk[per[d]["k"]].append(per[d]["g"])
     out = {}
-    for f, d in forms.items():
-        out[f] = {"pipe": d["ms_8waves"] / ref["ms_8waves"], "issue": d["ms_1wave"] / ref["ms_1wave"]}
-    # the counter's own weighting: SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU per form (per dispatch)
-    if micro_pmc:
-        acc = collections.defaultdict(lambda: collections.defaultdict(float))
-        for path in micro_pmc:
-            for row in csv.DictReader(open(path)):
-                k = row["Kernel_Name"].split("(")[0].strip()
-                acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
-        kname = {"v_mul_f32": "k_mul", "v_fma_f32": "k_fma", "v_mov_b32": "k_mov",
-                 "v_cndmask_b32": "k_cnd", "v_add_u32": "k_addu", "v_max3_f32": "k_max3",
-                 "v_cmp_lt_f32": "k_cmp", "v_sqrt_f32": "k_sqrt", "v_rcp_f32": "k_rcp",
-                 "v_div_scale_f32": "k_dsc", "v_div_fmas_f32": "k_dfm",
-                 "v_div_fixup_f32": "k_dfx", "v_mul_lo_u32": "k_mullo",
-                 "v_mul_hi_u32": "k_mulhi", "v_add_u32_dpp": "k_dpp",
-                 "v_mbcnt_lo_u32_b32": "k_mbcnt", "v_bfe_u32": "k_bfe", "v_fma_f64": "k_fma64",
-                 "v_mul_f64": "k_mul64", "v_add_f64": "k_add64", "v_lshl_add_u64": "k_lshl64",
-                 "v_rcp_f64": "k_rcp64", "v_pk_fma_f32": "k_pkfma", "v_pk_mul_f32": "k_pkmul",
-                 "v_pk_add_f32": "k_pkadd", "v_cvt_f64_f32": "k_cvt64",
-                 "v_readfirstlane_b32": "k_rfl", "s_add_u32": "k_salu", "mix_v_mul_s_add": "k_mix",
-                 "v_fmac_f32": "k_fmac", "v_max_f32": "k_max", "v_and_b32": "k_and",
-                 "v_lshlrev_b32": "k_lshl", "v_alignbit_b32": "k_align",
-                 "v_mul_f32_e64": "k_mule64", "v_sub_f32": "k_sub",
-                 "v_cndmask_b32_e64_sgpr": "k_cnds", "v_mul_f32_sgpr": "k_muls"}
-        for f, k in kname.items():
-            c = acc.get(k)
-            if f in out and c and c.get("SQ_INSTS_VALU"):
-                out[f]["counter_qc"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_INSTS_VALU"]
+    insts = 2048 * 8  # ITERS x 8 per wave
+
+    def mean(xs):  # GRBM_GUI_ACTIVE sums the 8 XCDs
+        return sum(xs) / len(xs) / 8.0
+
+    for k, g in byk.items():
+        if len(g) < 18:
+            continue
+        out[k] = {"w1": mean(g[1:6]) / insts, "w8": mean(g[7:12]) / (8 * insts),
+                  "w5": mean(g[13:18]) / (5 * insts)}
     return out
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--stats", required=True, help="stats-build render_once JSON (region counts)")
-    p.add_argument("--micro", required=True, help="tools/microbench_classes JSON")
-    p.add_argument("--micro-pmc", action="append", default=[],
-                   help="rocprofv3 counter_collection.csv of the microbenchmark (any number)")
+    p.add_argument("--micro-grbm", required=True,
+                   help="rocprofv3 counter_collection.csv (GRBM_GUI_ACTIVE) of microbench_classes")
     p.add_argument("--pmc", default=None,
                    help="JSON of the product frame's counters {name: value per dispatch}")
     p.add_argument("--hsaco", default=None)
@@ -124,93 +118,100 @@ def main():
     def entries(r):
         return waves if r < 0 else d[R.REGION_DEBUG_BASE + r]
 
-    costs = micro_costs(json.load(open(a.micro)), a.micro_pmc)
-    dyn = collections.Counter()      # class -> dynamic wave-instructions
-    mnem = collections.Counter()     # mnemonic -> dynamic wave-instructions
-    reg_dyn = collections.defaultdict(collections.Counter)  # region -> class -> dynamic
-    for _, mn, _, r in insts:
-        c = klass(mn)
-        if c is None:
+    mc = grbm_costs(a.micro_grbm)
+    cost5 = {c: mc[k]["w5"] for c, k in KERNEL.items()}
+    dyn = collections.Counter()
+    sub = collections.Counter()
+    mnem = collections.Counter()
+    reg = collections.defaultdict(collections.Counter)
+    for _, mn, ops, r in insts:
+        kc = klass(mn, ops)
+        if kc is None:
             continue
+        c, lab = kc
         n = entries(r)
         dyn[c] += n
-        mnem[mn] += n
-        reg_dyn[r][c] += n
-    lines = []
-    out = lines.append
-    out("Cycle attribution of %s (tools/cycle_attrib.py)" % a.kernel)
-    out("stats frame: %d segments, %d wave-iterations" % (st["segments"], d[0]))
-    out("")
-    out("Issue costs per class (tools/microbench_classes.hip, relative to v_mul_f32):")
-    out("  %-8s %-20s %6s %6s %8s" % ("class", "form", "pipe", "issue", "counter"))
-    for c in sorted(dyn, key=lambda c: -dyn[c]):
-        f = FORM[c]
-        k = costs.get(f, {})
-        out("  %-8s %-20s %6.2f %6.2f %8s" % (c, f, k.get("pipe", float("nan")),
-                                             k.get("issue", float("nan")),
-                                             "%.2f" % k["counter_qc"] if "counter_qc" in k
-                                             else "-"))
-    for f in ("v_mov_b32", "v_add_u32", "v_fmac_f32", "v_max_f32", "v_and_b32", "v_lshlrev_b32",
-              "v_sub_f32", "v_mul_f32_sgpr", "v_mul_f32_e64", "v_max3_f32", "v_alignbit_b32",
-              "v_rcp_f32", "v_div_fmas_f32", "v_div_fixup_f32", "v_mul_hi_u32",
-              "v_mbcnt_lo_u32_b32", "v_bfe_u32", "v_mul_f64", "v_add_f64", "v_pk_mul_f32",
-              "v_pk_add_f32", "mix_v_mul_s_add"):
-        if f in costs:
-            k = costs[f]
-            out("  %-8s %-20s %6.2f %6.2f %8s" % ("", f, k["pipe"], k["issue"],
-                                                 "%.2f" % k["counter_qc"] if "counter_qc" in k
-                                                 else "-"))
-    out("")
-    tot_i = sum(v for c, v in dyn.items() if c != "salu")
-    tot_pipe = sum(v * costs[FORM[c]]["pipe"] for c, v in dyn.items() if c != "salu")
-    tot_cnt = sum(v * costs[FORM[c]].get("counter_qc", costs[FORM[c]]["pipe"])
-                  for c, v in dyn.items() if c != "salu")
-    tot_issue = sum(v * costs[FORM[c]]["issue"] for c, v in dyn.items())
-    out("Dynamic mix of the frame (wave-instructions, from the attribution):")
-    out("  %-8s %14s %7s %16s %7s %16s %7s" % ("class", "instructions", "share", "pipe qcycles",
-                                              "share", "issue slots", "share"))
-    for c in sorted(dyn, key=lambda c: -dyn[c]):
-        v = dyn[c]
-        pc = 0.0 if c == "salu" else v * costs[FORM[c]]["pipe"]
-        ic = v * costs[FORM[c]]["issue"]
-        out("  %-8s %14.4g %6.1f%% %16.4g %6.1f%% %16.4g %6.1f%%" % (
-            c, v, 100 * v / (tot_i + dyn["salu"]), pc, 100 * pc / tot_pipe, ic,
-            100 * ic / tot_issue))
-    out("  VALU total %.4g wave-instructions; pipe-weighted %.4g quad-cycles (x%.3f); "
-        "counter-weighted %.4g; issue-weighted incl. SALU %.4g slots" % (
-            tot_i, tot_pipe, tot_pipe / tot_i, tot_cnt, tot_issue))
-    out("")
-    out("The most frequent mnemonics (dynamic):")
-    for m, v in mnem.most_common(25):
-        out("  %14.4g  %s" % (v, m))
-    out("")
-    out("Regions by issue-weighted slots (VALU by class cost + SALU):")
+        sub[(c, lab)] += n
+        mnem[(mn, c)] += n
+        reg[r][c] += n
+    valu = sum(v for c, v in dyn.items() if c != "salu")
+    pipe = {c: v * cost5[c] for c, v in dyn.items()}
+    valu_cyc = sum(v for c, v in pipe.items() if c != "salu")
+    nan = float("nan")
+    L = []
+    w = L.append
+    w("Cycle attribution of %s at C4 (tools/cycle_attrib.py)" % a.kernel)
+    w("stats frame: %d segments, %d wave-iterations, %d waves" % (st["segments"], d[0], waves))
+    w("")
+    w("Issue costs measured on the GPU (tools/microbench_classes.hip, GRBM_GUI_ACTIVE per")
+    w("dispatch): SIMD cycles per wave64 instruction, 8 independent chains per wave:")
+    w("  %-8s %-10s %10s %10s %10s" % ("class", "kernel", "1 wave", "5 waves", "8 waves"))
+    for c, k in KERNEL.items():
+        w("  %-8s %-10s %10.2f %10.2f %10.2f" % (c, k, mc[k]["w1"], mc[k]["w5"], mc[k]["w8"]))
+    w("  every form at 5 waves per SIMD:")
+    items = sorted(mc.items(), key=lambda kv: kv[1]["w5"])
+    for i in range(0, len(items), 6):
+        w("    " + ", ".join("%s %.2f" % (k, v["w5"]) for k, v in items[i:i + 6]))
+    w("")
+    w("Dynamic instruction mix of one C4 frame (wave64 instructions, from the attribution):")
+    w("  %-34s %14s %8s %16s %7s" % ("class / kind", "instructions", "of VALU", "VALU cycles",
+                                      "share"))
+    for (c, lab), v in sorted(sub.items(), key=lambda kv: -kv[1]):
+        cy = v * cost5[c]
+        is_v = c != "salu"
+        w("  %-34s %14.4g %7.1f%% %16.4g %6.1f%%" % (
+            c + " / " + lab, v, 100.0 * v / valu if is_v else nan, cy if is_v else nan,
+            100.0 * cy / valu_cyc if is_v else nan))
+    w("  VALU: %.4g instructions, %.4g SIMD cycles at the 5-wave costs (%.2f per instruction);"
+      % (valu, valu_cyc, valu_cyc / valu))
+    w("  SALU: %.4g instructions, %.4g cycles of the scalar unit" % (dyn["salu"],
+                                                                    pipe.get("salu", 0.0)))
+    w("")
+    w("The most frequent instructions (dynamic, class):")
+    for (mn, c), v in mnem.most_common(24):
+        w("  %14.4g  %-28s %s" % (v, mn, c))
+    w("")
+    w("Regions by VALU cycles (5-wave costs):")
     rows = []
-    for r, cc in reg_dyn.items():
-        slots = sum(v * costs[FORM[c]]["issue"] for c, v in cc.items())
-        pipe = sum(v * costs[FORM[c]]["pipe"] for c, v in cc.items() if c != "salu")
-        rows.append((slots, pipe, r, cc))
-    rows.sort(reverse=True)
-    for slots, pipe, r, cc in rows[:30]:
-        top = ", ".join("%s %.3g" % (c, v) for c, v in cc.most_common(4))
-        out("  %12.4g %5.1f%%  pipe %12.4g  %-34s %s" % (slots, 100 * slots / tot_issue, pipe,
-                                                     label(r), top))
+    for r, cc in reg.items():
+        cy = sum(v * cost5[c] for c, v in cc.items() if c != "salu")
+        rows.append((cy, r, cc))
+    rows.sort(key=lambda t: -t[0])
+    for cy, r, cc in rows[:28]:
+        mix = ", ".join("%s %.3g" % (c, v) for c, v in cc.most_common(4))
+        w("  %12.4g %5.1f%%  %-34s %s" % (cy, 100.0 * cy / valu_cyc, label(r), mix))
     if a.pmc:
         pm = json.load(open(a.pmc))
-        out("")
-        out("Against the product frame's counters (%s):" % a.pmc)
-        for k in sorted(pm):
-            out("  %-22s %.4g" % (k, pm[k]))
-        if "SQ_INSTS_VALU" in pm:
-            out("  attributed VALU / SQ_INSTS_VALU = %.4f" % (tot_i / pm["SQ_INSTS_VALU"]))
-        if "SQ_ACTIVE_INST_VALU" in pm:
-            out("  pipe-weighted / SQ_ACTIVE_INST_VALU = %.4f; counter-weighted / "
-                "SQ_ACTIVE_INST_VALU = %.4f" % (tot_pipe / pm["SQ_ACTIVE_INST_VALU"],
-                                                tot_cnt / pm["SQ_ACTIVE_INST_VALU"]))
-        if "SQ_ACTIVE_INST_VALU" in pm and "SQ_INSTS_SALU" in pm:
-            out("  issue-weighted (VALU + SALU) / (SQ_ACTIVE_INST_VALU + SQ_INSTS_SALU) = %.4f" %
-                (tot_issue / (pm["SQ_ACTIVE_INST_VALU"] + pm["SQ_INSTS_SALU"])))
-    text = "\n".join(lines)
+        simd_cycles = 1024 * pm["GRBM_GUI_ACTIVE"] / 8.0
+        w("")
+        w("Against the product frame (PMC per dispatch, %s):" % os.path.basename(a.pmc))
+        w("  GRBM_GUI_ACTIVE / 8 = %.4g cycles per XCD; x 1024 SIMDs = %.4g SIMD cycles" % (
+            pm["GRBM_GUI_ACTIVE"] / 8.0, simd_cycles))
+        w("  SQ_INSTS_VALU %.4g (attributed %.4g, ratio %.4f); SQ_INSTS_SALU %.4g (attributed"
+          " %.4g, ratio %.4f)" % (pm["SQ_INSTS_VALU"], valu, valu / pm["SQ_INSTS_VALU"],
+                                  pm["SQ_INSTS_SALU"], dyn["salu"],
+                                  dyn["salu"] / pm["SQ_INSTS_SALU"]))
+        w("  SQ_ACTIVE_INST_VALU %.4g quad-cycles = %.4g cycles = %.3f of the SIMD cycles: the"
+          % (pm["SQ_ACTIVE_INST_VALU"], 4 * pm["SQ_ACTIVE_INST_VALU"],
+             4 * pm["SQ_ACTIVE_INST_VALU"] / simd_cycles))
+        w("    counter gives one quad-cycle to each instruction of the fast and normal classes"
+          " alike (microbenchmark: SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU = 1.00 for both, 2.00 for")
+        w("    v_sqrt / v_rcp, 4.00 for v_rcp_f64), so it cannot tell the double-rate forms apart")
+        w("  VALU cycles by the measured class costs: %.4g = %.3f of the SIMD cycles" % (
+            valu_cyc, valu_cyc / simd_cycles))
+        sa = pipe.get("salu", 0.0)
+        w("  SALU cycles by the measured scalar cost: %.4g = %.3f of the SIMD cycles" % (
+            sa, sa / simd_cycles))
+        ref = 4 * (pm["SQ_ACTIVE_INST_VALU"] + pm["SQ_INSTS_SALU"])
+        w("  class-weighted VALU + SALU = %.4g cycles against (SQ_ACTIVE_INST_VALU + SQ_INSTS_SALU)"
+          " x 4 = %.4g: ratio %.4f" % (valu_cyc + sa, ref, (valu_cyc + sa) / ref))
+        if "SQ_WAVE_CYCLES" in pm:
+            w("  per wave: %.4g cycles alive; waiting on dependencies (SQ_WAIT_INST_ANY) %.3f,"
+              " issuing (SQ_ACTIVE_INST_ANY) %.3f of its life" % (
+                  4 * pm["SQ_WAVE_CYCLES"] / pm["SQ_WAVES"],
+                  pm.get("SQ_WAIT_INST_ANY", 0) / pm["SQ_WAVE_CYCLES"],
+                  pm.get("SQ_ACTIVE_INST_ANY", 0) / pm["SQ_WAVE_CYCLES"]))
+    text = "\n".join(L)
     print(text)
     if a.out:
         with open(a.out, "w") as f:

@@ -93,6 +93,16 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 #define F_ALIGN(r) "v_alignbit_b32 " r ", " r ", %8, 31\n"
 #define F_MULE64(r) "v_mul_f32_e64 " r ", " r ", %8\n"
 #define F_SUB(r) "v_sub_f32 " r ", " r ", %8\n"
+#define F_ADDF(r) "v_add_f32 " r ", " r ", %8\n"
+#define F_MIN(r) "v_min_f32 " r ", " r ", %8\n"
+#define F_OR(r) "v_or_b32 " r ", " r ", %8\n"
+#define F_XOR(r) "v_xor_b32 " r ", " r ", %8\n"
+#define F_LSHLV(r) "v_lshlrev_b32 " r ", %8, " r "\n"
+#define F_MULLIT(r) "v_mul_f32 " r ", 0x3f7fbe77, " r "\n"
+#define F_MED3(r) "v_med3_f32 " r ", " r ", %8, %8\n"
+#define F_CVTF32F64(r) "v_cvt_f32_f64 " r ", %9\n"
+#define F_CMPVCND(r) "v_cmp_lt_f32 vcc, " r ", %8\n v_cndmask_b32 " r ", " r ", %8, vcc\n"
+#define F_CMPSCND(r) "v_cmp_lt_f32 s[20:21], " r ", %8\n v_cndmask_b32_e64 " r ", " r ", %8, s[20:21]\n"
 
 K32(k_mul, F_MUL)
 K32(k_fma, F_FMA)
@@ -126,6 +136,79 @@ K32(k_lshl, F_LSHL)
 K32(k_align, F_ALIGN)
 K32(k_mule64, F_MULE64)
 K32(k_sub, F_SUB)
+K32(k_addf, F_ADDF)
+K32(k_min, F_MIN)
+K32(k_or, F_OR)
+K32(k_xor, F_XOR)
+K32(k_lshlv, F_LSHLV)
+K32(k_mullit, F_MULLIT)
+K32(k_med3, F_MED3)
+
+// the compiler's usual select: a compare into VCC (or an SGPR pair) and a v_cndmask reading it,
+// four independent (compare, select) pairs per group of eight instructions
+#define KCMP(NAME, FMT, ...)                                                                  \
+    __global__ void NAME(float* out, float s) {                                                \
+        float a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3;                         \
+        for (int i = 0; i < ITERS; i++) {                                                      \
+            asm volatile(FMT("%0") FMT("%1") FMT("%2") FMT("%3")                               \
+                         : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)                              \
+                         : "v"(s)                                                              \
+                         : __VA_ARGS__);                                                       \
+        }                                                                                      \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3;                        \
+    }
+#define F_CMPVCND4(r) "v_cmp_lt_f32 vcc, " r ", %4\n v_cndmask_b32 " r ", " r ", %4, vcc\n"
+#define F_CMPSCND4(r) "v_cmp_lt_f32 s[20:21], " r ", %4\n v_cndmask_b32_e64 " r ", " r ", %4, s[20:21]\n"
+KCMP(k_cmpvcnd, F_CMPVCND4, "vcc")
+KCMP(k_cmpscnd, F_CMPSCND4, "s20", "s21")
+
+// v_cndmask_b32 (VCC form) with VCC written by a compare before the loop
+__global__ void k_cndv(float* out, float s) {
+    float a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5,
+          a6 = a0 + 6, a7 = a0 + 7;
+    asm volatile("v_cmp_lt_f32 vcc, %0, %1\n s_nop 7" ::"v"(a0), "v"(s) : "vcc");
+    for (int i = 0; i < ITERS; i++) {
+        asm volatile(
+            "v_cndmask_b32 %0, %0, %8, vcc\n v_cndmask_b32 %1, %1, %8, vcc\n"
+            "v_cndmask_b32 %2, %2, %8, vcc\n v_cndmask_b32 %3, %3, %8, vcc\n"
+            "v_cndmask_b32 %4, %4, %8, vcc\n v_cndmask_b32 %5, %5, %8, vcc\n"
+            "v_cndmask_b32 %6, %6, %8, vcc\n v_cndmask_b32 %7, %7, %8, vcc\n"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "v"(s));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+// one dependent chain of v_mul_f32 (latency)
+__global__ void k_muldep(float* out, float s) {
+    float a0 = threadIdx.x;
+    for (int i = 0; i < ITERS; i++) {
+        asm volatile(
+            "v_mul_f32 %0, %0, %1\n v_mul_f32 %0, %0, %1\n v_mul_f32 %0, %0, %1\n"
+            "v_mul_f32 %0, %0, %1\n v_mul_f32 %0, %0, %1\n v_mul_f32 %0, %0, %1\n"
+            "v_mul_f32 %0, %0, %1\n v_mul_f32 %0, %0, %1\n"
+            : "+v"(a0)
+            : "v"(s));
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = a0;
+}
+
+// packed multiply by an SGPR pair (the linear scan's form)
+__global__ void k_pkmuls(float* out, float s) {
+    v2f a0 = {float(threadIdx.x), 1.f}, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+        a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+    const unsigned long long sv = ((unsigned long long)__float_as_uint(s) << 32) | __float_as_uint(s);
+    for (int i = 0; i < ITERS; i++) {
+        asm volatile(
+            "v_pk_mul_f32 %0, %0, %8\n v_pk_mul_f32 %1, %1, %8\n v_pk_mul_f32 %2, %2, %8\n"
+            "v_pk_mul_f32 %3, %3, %8\n v_pk_mul_f32 %4, %4, %8\n v_pk_mul_f32 %5, %5, %8\n"
+            "v_pk_mul_f32 %6, %6, %8\n v_pk_mul_f32 %7, %7, %8\n"
+            : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+            : "s"(sv));
+    }
+    v2f t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = t.x + t.y;
+}
 
 // v_cndmask_b32 on a lane mask in an SGPR pair set before the loop (the compiler's usual form)
 __global__ void k_cnds(float* out, float s) {
@@ -255,15 +338,21 @@ int main(int argc, char** argv) {
         {"v_lshlrev_b32", k_lshl, "valu32"},     {"v_alignbit_b32", k_align, "valu32"},
         {"v_mul_f32_e64", k_mule64, "valu32"},   {"v_sub_f32", k_sub, "valu32"},
         {"v_cndmask_b32_e64_sgpr", k_cnds, "valu32"}, {"v_mul_f32_sgpr", k_muls, "valu32"},
+        {"v_add_f32", k_addf, "valu32"},         {"v_min_f32", k_min, "valu32"},
+        {"v_or_b32", k_or, "valu32"},            {"v_xor_b32", k_xor, "valu32"},
+        {"v_lshlrev_b32_v", k_lshlv, "valu32"},  {"v_mul_f32_literal", k_mullit, "valu32"},
+        {"v_med3_f32", k_med3, "valu32"},        {"cmp_vcc_cndmask", k_cmpvcnd, "pair"},
+        {"cmp_sgpr_cndmask_e64", k_cmpscnd, "pair"}, {"v_cndmask_b32_vcc_set", k_cndv, "valu32"},
+        {"v_mul_f32_dependent", k_muldep, "valu32"}, {"v_pk_mul_f32_sgpr", k_pkmuls, "packed"},
     };
     const char* only = argc > 1 ? argv[1] : nullptr;  // one form (for a PMC run), or all
     std::printf("{\"cus\": %d, \"iters\": %d, \"forms\": [\n", cus, ITERS);
     bool first = true;
     for (const K& k : ks) {
         if (only && std::strcmp(only, k.name) != 0) continue;
-        double ms_at[2] = {0, 0};
-        const int wps[2] = {1, 8};  // waves per SIMD: 256-thread blocks are 4 waves (one/SIMD)
-        for (int w = 0; w < 2; w++) {
+        double ms_at[3] = {0, 0, 0};
+        const int wps[3] = {1, 8, 5};  // waves per SIMD: 256-thread blocks are 4 waves (one/SIMD)
+        for (int w = 0; w < 3; w++) {
             const int grid = cus * wps[w];
             hipLaunchKernelGGL(k.f, dim3(grid), dim3(256), 0, 0, out, 0.999f);
             hipEventRecord(e0);
@@ -278,10 +367,9 @@ int main(int argc, char** argv) {
         }
         // wave-instructions per SIMD of the timed loop: waves per SIMD x ITERS x 8
         std::printf("%s {\"form\": \"%s\", \"class\": \"%s\", \"ms_1wave\": %.5f, "
-                    "\"ms_8waves\": %.5f, \"insts_per_simd_1wave\": %d, "
-                    "\"insts_per_simd_8waves\": %d}",
-                    first ? " " : ",\n ", k.name, k.cls, ms_at[0], ms_at[1], ITERS * 8,
-                    8 * ITERS * 8);
+                    "\"ms_8waves\": %.5f, \"ms_5waves\": %.5f, \"insts_per_simd_1wave\": %d}",
+                    first ? " " : ",\n ", k.name, k.cls, ms_at[0], ms_at[1], ms_at[2],
+                    ITERS * 8);
         first = false;
     }
     std::printf("\n]}\n");
