@@ -1,0 +1,123 @@
+"""Seeded random configurations, bit for bit against the oracle (GPU).
+
+Each case draws a scene (clusters with nested, duplicate and hollow spheres, RTIOW-style grids,
+spheres on a line, scenes scaled far from unit size, a camera inside a glass sphere), a camera,
+a ragged frame size, spp, depth, kernel variant, work partition / quantum, an optional rank of a
+sharded frame and an optional second progressive frame. The product path (through the C ABI)
+must give the oracle's bits for every pixel it renders, and its segment count on one GPU. The
+reference loop these restate is shader.comp:42-57 over functions.glsl:65-92; the cases only
+widen the inputs the fixed-configuration tests (test_gpu_parity.py) cover.
+"""
+import numpy as np
+import pytest
+
+import vulkancomputeraytracing_amd as vc
+
+from tests.test_gpu_parity import assert_bitwise
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [vc.KERNEL_AUTO, vc.KERNEL_LDS, vc.KERNEL_SMEM, vc.KERNEL_CULL, vc.KERNEL_CULL_LANE,
+            vc.KERNEL_CULL_FLAT]
+
+
+def _material(rng):
+    m = int(rng.integers(1, 4))
+    param = {1: rng.uniform(0.0, 1.2), 2: rng.uniform(0.0, 1.0), 3: rng.uniform(1.1, 2.4)}[m]
+    return m, float(param)
+
+
+def _cluster(rng, n, spread):
+    rows = [((0.0, -1000.0, 0.0), 1000.0, (0.5, 0.5, 0.5), 1, 1.0)]
+    for i in range(n - 1):
+        c = tuple(float(v) for v in rng.uniform(-spread, spread, 3))
+        r = float(np.exp(rng.uniform(np.log(1e-3), np.log(0.3 * spread + 0.1))))
+        m, p = _material(rng)
+        rows.append((c, r, tuple(float(v) for v in rng.uniform(0, 1, 3)), m, p))
+        if i % 7 == 3:  # exact duplicate, other material: the lower index must win ties
+            rows.append((c, r, (1.0, 0.0, 0.0), 1 + m % 3, 0.5))
+        if i % 11 == 5:  # hollow glass shell inside it
+            rows.append((c, -0.8 * r, (1.0, 1.0, 1.0), 3, 1.5))
+    return rows
+
+
+def _line(rng, n):
+    # every centre on one line: degenerate (flat) hierarchy boxes
+    return [((float(x), 0.5, 0.0), float(rng.uniform(0.05, 0.45)),
+             tuple(float(v) for v in rng.uniform(0, 1, 3)), *_material(rng))
+            for x in np.linspace(-6, 6, n)]
+
+
+def make_case(oracle, seed):
+    rng = np.random.default_rng(1000 + seed)
+    kind = ["cluster", "cluster", "grid", "line", "scaled", "inside"][seed % 6]
+    look = (0.0, 0.5, 0.0)
+    if kind == "cluster":
+        rows = _cluster(rng, int(rng.integers(3, 400)), 3.0)
+        eye = tuple(float(v) for v in rng.uniform(-10, 10, 3))
+        eye = (eye[0], abs(eye[1]) + 0.5, eye[2] + 12.0)
+    elif kind == "grid":  # the reference generator's rules on a random grid size
+        o = oracle
+        half = int(rng.integers(2, 12))
+        sc = np.concatenate([o.random_spheres(-half, half), o.big_three_and_ground()])
+        rows = None
+        eye, look = (13.0, 2.0, 3.0), (0.0, 0.0, 0.0)
+    elif kind == "line":
+        rows = _line(rng, int(rng.integers(16, 120)))
+        eye = (float(rng.uniform(-3, 3)), float(rng.uniform(0.5, 4)), 9.0)
+    elif kind == "scaled":  # the same kind of cluster, far from unit scale
+        s = float(10.0 ** rng.uniform(-2, 3))
+        rows = [((c[0] * s, c[1] * s, c[2] * s), r * s, col, m, p)
+                for c, r, col, m, p in _cluster(rng, int(rng.integers(16, 200)), 3.0)]
+        eye, look = (4.0 * s, 3.0 * s, 12.0 * s), (0.0, 0.5 * s, 0.0)
+    else:  # the camera inside a big glass sphere among others
+        rows = _cluster(rng, int(rng.integers(16, 120)), 3.0)
+        rows.append(((0.0, 1.0, 6.0), 3.0, (1.0, 1.0, 1.0), 3, float(rng.uniform(1.1, 1.9))))
+        eye = (0.0, 1.0, 6.5)
+    if rows is not None:
+        sc = vc.make_spheres(rows)
+    w, h = int(rng.integers(1, 161)), int(rng.integers(1, 97))
+    spp, depth = int(rng.integers(1, 25)), int(rng.integers(1, 41))
+    variant = VARIANTS[int(rng.integers(0, len(VARIANTS)))]
+    chunk = quantum = 0
+    if rng.uniform() < 0.5:
+        quantum = int(2 ** rng.integers(0, 3))
+        chunk = quantum * int(rng.integers(1, 4))
+    world = [1, 1, 1, 2, 3, 8][int(rng.integers(0, 6))]
+    rank = int(rng.integers(0, world))
+    frames = 2 if rng.uniform() < 0.25 else 1
+    cam = dict(lookfrom=eye, lookat=look, vfov=float(rng.uniform(8, 100)))
+    return dict(kind=kind, scene=sc, w=w, h=h, spp=spp, depth=depth, variant=variant,
+                chunk=chunk, quantum=quantum, world=world, rank=rank, frames=frames, cam=cam)
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_random_configuration_bitwise(oracle, seed):
+    c = make_case(oracle, seed)
+    what = (f"seed {seed} {c['kind']} n{len(c['scene'])} {c['w']}x{c['h']} spp{c['spp']} "
+            f"d{c['depth']} v{c['variant']} k{c['chunk']}/q{c['quantum']} "
+            f"rank {c['rank']}/{c['world']} frames {c['frames']}")
+    desc = vc.RenderDesc(width=c["w"], height=c["h"], samples_per_pixel=c["spp"],
+                         max_depth=c["depth"], kernel_variant=c["variant"], device=0,
+                         rank=c["rank"], world_size=c["world"], accumulate_chunk=c["chunk"],
+                         accumulate_quantum=c["quantum"], progressive=c["frames"] > 1,
+                         **c["cam"])
+    with vc.Renderer(desc, c["scene"]) as r:
+        for _ in range(c["frames"]):
+            r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    spp_total = c["spp"] * c["frames"]
+    cfg = oracle.config(c["w"], c["h"], spp_total, c["depth"], **oracle.partition(st),
+                        frame_spp=c["spp"] if c["frames"] > 1 else 0, **c["cam"])
+    want, segs = oracle.render(cfg, c["scene"])
+    if c["world"] == 1:
+        assert_bitwise(got, want, what)
+        if c["frames"] == 1:
+            assert st["segments"] == segs, what
+    else:
+        m = vc.tile_pixel_map(c["w"], c["h"], c["world"])
+        mine = m[..., 0] == c["rank"]
+        ntiles = len(vc.tiles_for_rank(c["w"], c["h"], c["world"], c["rank"]))
+        assert got.shape == (ntiles, 64, 4), what
+        if mine.any():
+            assert_bitwise(got.reshape(-1, 4)[m[..., 1][mine]], want[mine], what)

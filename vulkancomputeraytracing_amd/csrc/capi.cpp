@@ -967,9 +967,11 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
         g.local_pixels += std::min<uint64_t>(8, g.desc.width - 8 * tx) *
                           std::min<uint64_t>(8, g.desc.height - 8 * ty);
     }
-    if (g.fb_bytes) {  // sharded: padded to the largest rank, the size every rank sends
-        const size_t own = g.desc.world_size == 1 ? g.fb_bytes
-                                                  : static_cast<size_t>(g.pad_tiles) * 64 * 16;
+    // sharded: padded to the largest rank, the size every rank sends -- also a rank that owns
+    // no tile (a frame of fewer tiles than ranks) sends that many zero bytes to the gather
+    const size_t own = g.desc.world_size == 1 ? g.fb_bytes
+                                              : static_cast<size_t>(g.pad_tiles) * 64 * 16;
+    if (own) {
         if ((r = to_vk(hipMalloc(&g.d_fb_own, own))) != VK_SUCCESS) return fail(r);
         if ((r = to_vk(hipMemset(g.d_fb_own, 0, own))) != VK_SUCCESS) return fail(r);
     }
