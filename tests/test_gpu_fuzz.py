@@ -48,8 +48,8 @@ def _line(rng, n):
             for x in np.linspace(-6, 6, n)]
 
 
-def make_case(oracle, seed):
-    rng = np.random.default_rng(1000 + seed)
+def make_case(oracle, seed, bright=False):
+    rng = np.random.default_rng((2000 if bright else 1000) + seed)
     kind = ["cluster", "cluster", "grid", "line", "scaled", "inside"][seed % 6]
     look = (0.0, 0.5, 0.0)
     if kind == "cluster":
@@ -74,6 +74,12 @@ def make_case(oracle, seed):
         rows = _cluster(rng, int(rng.integers(16, 120)), 3.0)
         rows.append(((0.0, 1.0, 6.0), 3.0, (1.0, 1.0, 1.0), 3, float(rng.uniform(1.1, 1.9))))
         eye = (0.0, 1.0, 6.5)
+    if bright and rows is not None:
+        # Lambertian "reflect ratios" above 1 (textures.glsl:22 multiplies them in): radiance
+        # grows with depth, so quantum sums leave the 2^32 scale and the per-pixel scale and
+        # the re-render run (vcrt_math.h "Accumulation")
+        rows = [(c, r, tuple(0.7 + 0.3 * v for v in col), m, float(rng.uniform(3.0, 4.5)))
+                if m == 1 else (c, r, col, m, p) for c, r, col, m, p in rows]
     if rows is not None:
         sc = vc.make_spheres(rows)
     w, h = int(rng.integers(1, 161)), int(rng.integers(1, 97))
@@ -86,14 +92,16 @@ def make_case(oracle, seed):
     world = [1, 1, 1, 2, 3, 8][int(rng.integers(0, 6))]
     rank = int(rng.integers(0, world))
     frames = 2 if rng.uniform() < 0.25 else 1
-    cam = dict(lookfrom=eye, lookat=look, vfov=float(rng.uniform(8, 100)))
+    vup = (0.0, 1.0, 0.0) if rng.uniform() < 0.7 else tuple(float(v) for v in rng.uniform(-1, 1, 3))
+    if abs(float(np.dot(vup, np.subtract(eye, look)))) > 0.99 * float(
+            np.linalg.norm(vup) * np.linalg.norm(np.subtract(eye, look))):
+        vup = (0.0, 1.0, 0.0)  # (vup parallel to the view axis: no camera basis)
+    cam = dict(lookfrom=eye, lookat=look, vup=vup, vfov=float(rng.uniform(8, 100)))
     return dict(kind=kind, scene=sc, w=w, h=h, spp=spp, depth=depth, variant=variant,
                 chunk=chunk, quantum=quantum, world=world, rank=rank, frames=frames, cam=cam)
 
 
-@pytest.mark.parametrize("seed", range(120))
-def test_random_configuration_bitwise(oracle, seed):
-    c = make_case(oracle, seed)
+def check_case(oracle, c, seed):
     what = (f"seed {seed} {c['kind']} n{len(c['scene'])} {c['w']}x{c['h']} spp{c['spp']} "
             f"d{c['depth']} v{c['variant']} k{c['chunk']}/q{c['quantum']} "
             f"rank {c['rank']}/{c['world']} frames {c['frames']}")
@@ -121,3 +129,22 @@ def test_random_configuration_bitwise(oracle, seed):
         assert got.shape == (ntiles, 64, 4), what
         if mine.any():
             assert_bitwise(got.reshape(-1, 4)[m[..., 1][mine]], want[mine], what)
+    return st
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_random_configuration_bitwise(oracle, seed):
+    check_case(oracle, make_case(oracle, seed), seed)
+
+
+def test_random_bright_configurations_bitwise(oracle):
+    """40 of the cases with bright Lambertians (albedo 0.7-1, ratio 3-4.5, the ground too): the
+    pixels whose quantum sums leave the first scale re-render at their own (vcrt_math.h
+    "Accumulation"), on every variant, partition, rank and progressive frame; several cases
+    must take that path."""
+    rerenders = 0
+    for seed in range(40):
+        c = make_case(oracle, seed, bright=True)
+        c["depth"] = max(c["depth"], 16)
+        rerenders += check_case(oracle, c, seed)["scale_rerenders"] > 0
+    assert rerenders >= 3, rerenders
