@@ -48,11 +48,16 @@ def _line(rng, n):
             for x in np.linspace(-6, 6, n)]
 
 
-def make_case(oracle, seed, bright=False):
-    rng = np.random.default_rng((2000 if bright else 1000) + seed)
-    kind = ["cluster", "cluster", "grid", "line", "scaled", "inside"][seed % 6]
+def make_case(oracle, seed, bright=False, big=False):
+    rng = np.random.default_rng((3000 if big else 2000 if bright else 1000) + seed)
+    kind = "big" if big else ["cluster", "cluster", "grid", "line", "scaled", "inside"][seed % 6]
     look = (0.0, 0.5, 0.0)
-    if kind == "cluster":
+    if kind == "big":  # many hierarchy chunks; tables beyond LDS (boxes-only and global kernels)
+        rows = _cluster(rng, int(rng.integers(600, 5000)), 20.0)
+        eye = tuple(float(v) for v in rng.uniform(-25, 25, 3))
+        eye = (eye[0], abs(eye[1]) + 0.5, eye[2])
+        look = tuple(float(v) for v in rng.uniform(-5, 5, 3))
+    elif kind == "cluster":
         rows = _cluster(rng, int(rng.integers(3, 400)), 3.0)
         eye = tuple(float(v) for v in rng.uniform(-10, 10, 3))
         eye = (eye[0], abs(eye[1]) + 0.5, eye[2] + 12.0)
@@ -84,6 +89,8 @@ def make_case(oracle, seed, bright=False):
         sc = vc.make_spheres(rows)
     w, h = int(rng.integers(1, 161)), int(rng.integers(1, 97))
     spp, depth = int(rng.integers(1, 25)), int(rng.integers(1, 41))
+    if big:  # (the oracle's linear scan: small frames)
+        w, h, spp = int(rng.integers(1, 49)), int(rng.integers(1, 33)), int(rng.integers(1, 5))
     variant = VARIANTS[int(rng.integers(0, len(VARIANTS)))]
     chunk = quantum = 0
     if rng.uniform() < 0.5:
@@ -135,6 +142,11 @@ def check_case(oracle, c, seed):
 @pytest.mark.parametrize("seed", range(120))
 def test_random_configuration_bitwise(oracle, seed):
     check_case(oracle, make_case(oracle, seed), seed)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_large_scene_configuration_bitwise(oracle, seed):
+    check_case(oracle, make_case(oracle, seed, big=True), seed)
 
 
 def test_random_bright_configurations_bitwise(oracle):
