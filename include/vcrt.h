@@ -82,7 +82,9 @@ typedef struct vcrt_camera { /* globals.glsl:21-24 */
 
 typedef struct vcrt_render_desc {
     uint32_t struct_size;      /* sizeof(vcrt_render_desc) */
-    int32_t width, height;     /* IMAGE_WIDTH, IMAGE_HEIGHT */
+    int32_t width, height;     /* IMAGE_WIDTH, IMAGE_HEIGHT: each <= 65535; a rank's 8x8 tiles
+                                * hold <= 2^26 pixels (8192 x 8192 on one GPU), else vcrt_begin
+                                * returns VCRT_ERROR_FORMAT_NOT_SUPPORTED */
     int32_t samples_per_pixel; /* SAMPLES_PER_PIXEL, >= 1 */
     int32_t max_depth;         /* MAX_RECURSION_LEVEL, >= 0 */
     vcrt_camera camera;

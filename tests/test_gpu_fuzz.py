@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import vulkancomputeraytracing_amd as vc
+from vulkancomputeraytracing_amd import _native as N
 
 from tests.test_gpu_parity import assert_bitwise
 
@@ -160,3 +161,35 @@ def test_random_bright_configurations_bitwise(oracle):
         c["depth"] = max(c["depth"], 16)
         rerenders += check_case(oracle, c, seed)["scale_rerenders"] > 0
     assert rerenders >= 3, rerenders
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [(65535, 3, 2, 4),     # the widest frame (x in 16 bits)
+                                           (5, 65535, 2, 4),     # the tallest
+                                           (8192, 8192, 8, 3)])  # 2^26 pixels, summed quanta
+def test_extreme_frame_shapes_bitwise(oracle, w, h, spp, depth):
+    """Frames at the C ABI's size limits (vcrt.h: width, height <= 65535, <= 2^26 pixels in a
+    rank's tiles): rows spread over the frame, bitwise against the oracle's render of the same
+    rows; one tile more than 2^26 pixels is refused at vcrt_begin."""
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0)
+    with vc.Renderer(desc, "final") as r:
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    assert got.shape == (h, w, 4)
+    cfg = oracle.config(w, h, spp, depth, **oracle.partition(st))
+    for y in sorted({0, h // 3, h // 2, h - 1}):
+        xy = np.stack([np.arange(w), np.full(w, y)], axis=1)
+        want, _ = oracle.render_pixels(cfg, oracle.scene("final"), xy)
+        assert_bitwise(got[y], want, f"{w}x{h} row {y}")
+
+
+def test_frame_beyond_the_slot_limit_is_refused():
+    # 8200 x 8192: 1025 x 1024 tiles of 64 slots > 2^26 (vcrt.h vcrt_render_desc)
+    desc = vc.RenderDesc(width=8200, height=8192, samples_per_pixel=8, max_depth=3, device=0)
+    with pytest.raises(vc.VcrtError) as e:
+        with vc.Renderer(desc, "final"):
+            pass
+    assert e.value.code == N.VK_ERROR_FORMAT_NOT_SUPPORTED
+    # the same frame in four shards fits every rank
+    with vc.Renderer(vc.RenderDesc(width=8200, height=8192, samples_per_pixel=1, max_depth=1,
+                                   device=0, rank=3, world_size=4), "final") as r:
+        r.draw_next_frame()

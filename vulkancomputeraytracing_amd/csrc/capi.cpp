@@ -568,16 +568,24 @@ VkResult launch(hipFunction_t f, uint32_t grid, uint32_t block, uint32_t lds, Pa
 }
 
 // Zero the pixels' sums and their outlier record (a new scene, vcrt_begin, a reset): every
-// pixel starts again at the scale 2^32 (vcrt_math.h "Accumulation").
+// pixel starts again at the scale 2^32 (vcrt_math.h "Accumulation"). On the render stream, and
+// waited for: the render stream is non-blocking, so a memset on the null stream would not be
+// ordered before the next frame's kernels (a 2-GiB memset still running then zeroed the last
+// rows' sums of an 8192 x 8192 frame).
 hipError_t reset_sums() {
     if (g.d_accum) {
-        const hipError_t e = hipMemset(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels));
+        const hipError_t e = hipMemsetAsync(g.d_accum, 0, 32u * static_cast<size_t>(g.total_pixels),
+                                            g.stream);
         if (e != hipSuccess) return e;
         g.accum_clean = true;
     }
     if (g.d_pixel_emax) {
-        const hipError_t e =
-            hipMemset(g.d_pixel_emax, 0, sizeof(uint32_t) * static_cast<size_t>(g.total_pixels));
+        const hipError_t e = hipMemsetAsync(
+            g.d_pixel_emax, 0, sizeof(uint32_t) * static_cast<size_t>(g.total_pixels), g.stream);
+        if (e != hipSuccess) return e;
+    }
+    if (g.stream) {
+        const hipError_t e = hipStreamSynchronize(g.stream);
         if (e != hipSuccess) return e;
     }
     g.pixel_scale = false;
@@ -953,6 +961,10 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     // Frame sharding: 8x8 tiles, (tx, ty) to rank (tx + ty) % world (DESIGN.md "Multi-GPU").
     g.tiles_x = static_cast<uint32_t>((g.desc.width + 7) / 8);
     g.local_tiles = tiles_for_rank(g.desc.width, g.desc.height, g.desc.world_size, g.desc.rank);
+    // a lane keeps its item's slot in the low kRingQBits bits of one register (the ring entry
+    // above it): at most 2^26 slots per rank (8192 x 8192 on one GPU)
+    if (static_cast<uint64_t>(g.local_tiles) * 64u > (uint64_t{1} << vcrt::kRingQBits))
+        return fail(VCRT_ERROR_FORMAT_NOT_SUPPORTED);
     g.local_elems = g.desc.world_size == 1
                         ? static_cast<uint32_t>(g.desc.width) * static_cast<uint32_t>(g.desc.height)
                         : g.local_tiles * 64u;
@@ -973,7 +985,8 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
                                               : static_cast<size_t>(g.pad_tiles) * 64 * 16;
     if (own) {
         if ((r = to_vk(hipMalloc(&g.d_fb_own, own))) != VK_SUCCESS) return fail(r);
-        if ((r = to_vk(hipMemset(g.d_fb_own, 0, own))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemsetAsync(g.d_fb_own, 0, own, g.stream))) != VK_SUCCESS)
+            return fail(r);
     }
     g.d_fb = g.d_fb_own;
     // Work decomposition: (local tile, chunk of K samples) items holding whole quanta; a pixel's
@@ -1010,11 +1023,13 @@ vcrt_result vcrt_begin(const vcrt_render_desc* desc) {
     if (!g.direct && g.total_pixels) {  // 32 B per pixel, whatever the spp
         const size_t bytes = 32u * static_cast<size_t>(g.total_pixels);
         if ((r = to_vk(hipMalloc(&g.d_accum, bytes))) != VK_SUCCESS) return fail(r);
-        if ((r = to_vk(hipMemset(g.d_accum, 0, bytes))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemsetAsync(g.d_accum, 0, bytes, g.stream))) != VK_SUCCESS)
+            return fail(r);
         g.accum_clean = true;
         const size_t eb = sizeof(uint32_t) * static_cast<size_t>(g.total_pixels);
         if ((r = to_vk(hipMalloc(&g.d_pixel_emax, eb))) != VK_SUCCESS) return fail(r);
-        if ((r = to_vk(hipMemset(g.d_pixel_emax, 0, eb))) != VK_SUCCESS) return fail(r);
+        if ((r = to_vk(hipMemsetAsync(g.d_pixel_emax, 0, eb, g.stream))) != VK_SUCCESS)
+            return fail(r);
     }
     if ((r = to_vk(hipMalloc(&g.d_counters, kCounterBytes))) != VK_SUCCESS) return fail(r);
     if ((r = to_vk(hipHostMalloc(&g.h_counters, 4 * sizeof(unsigned long long)))) != VK_SUCCESS)
@@ -1197,6 +1212,8 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
         VCRT_TRY(
             hipMemcpy(g.d_material, mat.data(), sizeof(float4) * count, hipMemcpyHostToDevice));
     }
+    // (the uploads above ran on the null stream; the render stream does not wait for it)
+    VCRT_TRY(hipStreamSynchronize(nullptr));
     g.nspheres = count;
     g.stats.nspheres = count;
     g.accumulated = 0;  // a new scene restarts progressive accumulation
@@ -1281,6 +1298,7 @@ VkResult build_block_order(uint32_t total_blocks) {
     }
     VCRT_TRY(hipMemcpy(g.d_block_order, order.data(), total_blocks * sizeof(uint32_t),
                        hipMemcpyHostToDevice));
+    VCRT_TRY(hipStreamSynchronize(nullptr));  // before the render stream's next frame reads it
     return VK_SUCCESS;
 }
 
@@ -1740,10 +1758,11 @@ vcrt_result vcrt_comm_init(const vcrt_comm_id* id) {
         const size_t slab = static_cast<size_t>(g.pad_tiles) * 64 * sizeof(float4);
         const size_t all = slab * static_cast<size_t>(g.desc.world_size);
         if ((err = hipMalloc(&g.d_gather, all)) != hipSuccess) return fail(err);
-        if ((err = hipMemset(g.d_gather, 0, all)) != hipSuccess) return fail(err);
+        if ((err = hipMemsetAsync(g.d_gather, 0, all, g.stream)) != hipSuccess) return fail(err);
         const size_t frame = static_cast<size_t>(g.desc.width) * g.desc.height * sizeof(float4);
         if ((err = hipMalloc(&g.d_frame, frame)) != hipSuccess) return fail(err);
-        if ((err = hipMemset(g.d_frame, 0, frame)) != hipSuccess) return fail(err);
+        if ((err = hipMemsetAsync(g.d_frame, 0, frame, g.stream)) != hipSuccess) return fail(err);
+        if ((err = hipStreamSynchronize(g.stream)) != hipSuccess) return fail(err);
         g.d_fb = g.d_gather;  // rank 0 renders straight into its slot of the gather buffer
     } else {
         g.d_fb = g.d_fb_own;
@@ -1828,6 +1847,7 @@ vcrt_result vcrt_selftest_sin(uint32_t first, uint32_t count, uint64_t* mismatch
     VCRT_TRY(hipMalloc(&buf, 24));
     uint32_t init[6] = {0, 0, 0, 0, 0xFFFFFFFFu, 0};
     hipError_t e = hipMemcpy(buf, init, sizeof(init), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // (the check runs on g.stream)
     vcrt::SinCheckParams sp{static_cast<unsigned long long*>(buf),
                             reinterpret_cast<uint32_t*>(static_cast<char*>(buf) + 16), first, count,
                             {}};
