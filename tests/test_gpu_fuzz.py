@@ -193,3 +193,80 @@ def test_frame_beyond_the_slot_limit_is_refused():
     with vc.Renderer(vc.RenderDesc(width=8200, height=8192, samples_per_pixel=1, max_depth=1,
                                    device=0, rank=3, world_size=4), "final") as r:
         r.draw_next_frame()
+
+
+def _same_bits_or_both_nan(got, want, what):
+    g, w = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    both_nan = np.isnan(g) & np.isnan(w)
+    gb, wb = g.view(np.uint32).copy(), w.view(np.uint32).copy()
+    gb[both_nan] = wb[both_nan] = 0
+    assert_bitwise(gb.view(np.float32), wb.view(np.float32), what)
+
+
+@pytest.mark.parametrize("case", ["huge_radius", "nan_centre", "zero_radius", "wide_fov",
+                                  "narrow_fov", "eye_on_target", "many_samples", "deep"])
+def test_edge_inputs_bitwise(oracle, case):
+    """Inputs at the edge of the reference's arithmetic: a sphere too large for the culling
+    guard (the linear scan then), a NaN centre (never hit), a zero radius, fields of view of 170
+    and 0.5 degrees, the camera on its target (normalize(0) gives a NaN basis; hit_sphere's
+    `disc < 0` rejection lets a NaN ray through, so every segment "hits" and the path ends at
+    the depth limit with the canonical black), 2^16 samples (quantum 128: 512 quanta per pixel)
+    and depth 500."""
+    rows = [((0.0, -1000.0, 0.0), 1000.0, (0.5, 0.5, 0.5), 1, 1.0),
+            ((0.0, 1.0, 0.0), 1.0, (1.0, 1.0, 1.0), 3, 1.5),
+            ((-4.0, 1.0, 0.0), 1.0, (0.4, 0.2, 0.1), 1, 1.0),
+            ((4.0, 1.0, 0.0), 1.0, (0.7, 0.6, 0.5), 2, 0.0)]
+    rng = np.random.default_rng(7)
+    for i in range(20):
+        rows.append(((float(rng.uniform(-6, 6)), 0.2, float(rng.uniform(-6, 6))), 0.2,
+                     tuple(float(v) for v in rng.uniform(0, 1, 3)), 1 + i % 3, 0.5))
+    cam = dict(lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0), vfov=20.0)
+    w, h, spp, depth = 48, 27, 4, 10
+    if case == "huge_radius":
+        rows.append(((0.0, 0.0, -3e9), 2.9e9, (0.9, 0.9, 0.9), 1, 0.8))
+    elif case == "nan_centre":
+        rows.append(((float("nan"), 1.0, 0.0), 0.5, (1.0, 0.0, 0.0), 1, 1.0))
+    elif case == "zero_radius":
+        rows.append(((1.0, 0.5, 1.0), 0.0, (1.0, 0.0, 0.0), 2, 0.0))
+    elif case == "wide_fov":
+        cam["vfov"] = 170.0
+    elif case == "narrow_fov":
+        cam["vfov"] = 0.5
+    elif case == "eye_on_target":
+        cam["lookat"] = cam["lookfrom"]
+    elif case == "many_samples":
+        w, h, spp, depth = 3, 2, 1 << 16, 6
+    elif case == "deep":
+        w, h, spp, depth = 16, 9, 4, 500
+    sc = vc.make_spheres(rows)
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         **cam)
+    with vc.Renderer(desc, sc) as r:
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st), **cam), sc)
+    _same_bits_or_both_nan(got, want, case)
+    assert st["segments"] == segs
+    if case == "eye_on_target":  # every NaN ray "hits" and its path ends at the depth limit
+        assert segs == w * h * spp * depth and (got[..., :3] == 0).all()
+
+
+def test_progressive_limit_is_refused_cleanly(oracle):
+    """Progressive frames add quanta to each pixel's exact sums, at most 512 (vcrt_math.h
+    kAccumMaxChunks): with 64 spp in quanta of 4, frame 33 is refused, and the frame read back
+    is still frame 32's, equal to the oracle's 2048-sample image."""
+    w, h, spp, depth = 16, 9, 64, 6
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         progressive=True)
+    with vc.Renderer(desc, "final") as r:
+        k = oracle.partition(r.stats())
+        for _ in range(32):
+            r.draw_next_frame()
+        with pytest.raises(vc.VcrtError) as e:
+            r.draw_next_frame()
+        assert e.value.code == N.VK_ERROR_FORMAT_NOT_SUPPORTED
+        got = r.read_framebuffer()
+        assert r.stats()["accumulated_spp"] == 32 * spp
+    want, _ = oracle.render(oracle.config(w, h, 32 * spp, depth, **k, frame_spp=spp),
+                            oracle.scene("final"))
+    assert_bitwise(got, want, "frame 32")
