@@ -270,3 +270,37 @@ def test_progressive_limit_is_refused_cleanly(oracle):
     want, _ = oracle.render(oracle.config(w, h, 32 * spp, depth, **k, frame_spp=spp),
                             oracle.scene("final"))
     assert_bitwise(got, want, "frame 32")
+
+
+def test_scene_switch_and_reset_on_a_large_frame(oracle):
+    """A 4096 x 2304 progressive renderer (600 MB of sums): two frames of the final scene, a
+    switch to the three-sphere scene (another kernel; the sums restart), a frame, a reset and a
+    frame of the final scene again: each read-back equals the oracle on spread rows (the
+    stream-ordered resets of this round: a reset still running under a frame would zero some
+    of its pixels)."""
+    w, h, spp, depth = 4096, 2304, 8, 4
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         progressive=True)
+    rows = [0, 777, 1500, h - 1]
+
+    def check(got, scene, frames, what, k):
+        cfg = oracle.config(w, h, frames * spp, depth, **k, frame_spp=spp)
+        for y in rows:
+            xy = np.stack([np.arange(w), np.full(w, y)], axis=1)
+            want, _ = oracle.render_pixels(cfg, oracle.scene(scene), xy)
+            assert_bitwise(got[y], want, f"{what} row {y}")
+
+    with vc.Renderer(desc, "final") as r:
+        k = oracle.partition(r.stats())
+        r.draw_next_frame()
+        r.draw_next_frame()
+        check(r.read_framebuffer(), "final", 2, "final x2", k)
+        r.set_scene(oracle.scene("three"))
+        r.draw_next_frame()
+        assert r.stats()["kernel"].startswith("vcrt_trace_smem")
+        check(r.read_framebuffer(), "three", 1, "three", k)
+        r.set_scene(oracle.scene("final"))
+        r.draw_next_frame()
+        r.reset_accumulation()
+        r.draw_next_frame()
+        check(r.read_framebuffer(), "final", 1, "final after reset", k)

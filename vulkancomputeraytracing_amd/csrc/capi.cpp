@@ -1216,7 +1216,13 @@ vcrt_result vcrt_set_scene(const vcrt_sphere* spheres, int32_t count) {
     VCRT_TRY(hipStreamSynchronize(nullptr));
     g.nspheres = count;
     g.stats.nspheres = count;
-    g.accumulated = 0;  // a new scene restarts progressive accumulation
+    if (g.desc.progressive && g.accumulated > 0) {
+        // a new scene restarts progressive accumulation at sample 0: the jitter table holds
+        // the last frame's sample indices
+        const VkResult rj = setup_jitter(0);
+        if (rj != VK_SUCCESS) return rj;
+    }
+    g.accumulated = 0;
     g.order_key = 0;    // and its cost order is measured again
     VCRT_TRY(reset_sums());
     g.scene_bounded = true;
