@@ -304,3 +304,23 @@ def test_scene_switch_and_reset_on_a_large_frame(oracle):
         r.reset_accumulation()
         r.draw_next_frame()
         check(r.read_framebuffer(), "final", 1, "final after reset", k)
+
+
+def test_a_replaced_renderer_is_stale(oracle):
+    """libvcrt holds one renderer per process (vcrt.h): a second Renderer's vcrt_begin ends the
+    first. The first object then raises instead of acting on the second's state, and closing it
+    leaves the second running."""
+    d = vc.RenderDesc(width=24, height=16, samples_per_pixel=2, max_depth=5, device=0)
+    r1 = vc.Renderer(d, "final")
+    r2 = vc.Renderer(d, "three")
+    with pytest.raises(vc.VcrtError):
+        r1.draw_next_frame()
+    r1.close()
+    r2.draw_next_frame()
+    got, st = r2.read_framebuffer(), r2.stats()
+    r2.close()
+    with pytest.raises(vc.VcrtError):
+        r2.stats()
+    want, _ = oracle.render(oracle.config(24, 16, 2, 5, **oracle.partition(st)),
+                            oracle.scene("three"))
+    assert_bitwise(got, want, "second renderer")

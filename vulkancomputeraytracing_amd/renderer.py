@@ -141,7 +141,21 @@ def SetRenderScene(spheres) -> int:
     return N.VK_SUCCESS
 
 
+# The C ABI holds one renderer per process (vcrt.h): a vcrt_begin ends the one before it. The
+# Renderer object that owns the current state; an older one is stale and its calls raise
+# instead of acting on its successor's state (or ending it on close).
+_live = None
+
+
+def _retire_live() -> None:
+    global _live
+    if _live is not None:
+        _live._open = False
+        _live = None
+
+
 def BeginRenderingOperation() -> int:
+    _retire_live()
     lib = N.lib()
     d = _desc.to_c()
     r = lib.vcrt_begin(ctypes.byref(d))
@@ -157,6 +171,7 @@ def DrawNextFrame() -> int:
 
 
 def EndRenderingOperation() -> int:
+    _retire_live()
     return N.lib().vcrt_end()
 
 
@@ -170,10 +185,20 @@ class Renderer:
         self._lib = N.lib()
         self._frame_stats = N.vcrt_stats()  # frame_times()' reused struct
         self._c_desc = self.desc.to_c()
+        _retire_live()  # vcrt_begin ends the previous renderer's state
         N.check("vcrt_begin", self._lib.vcrt_begin(ctypes.byref(self._c_desc)))
+        global _live
+        _live = self
         self._open = True
         if scene is not None:
             self.set_scene(scene)
+
+    def _L(self):
+        """The library, for the renderer that owns the C ABI's state; a stale one raises."""
+        if not getattr(self, "_open", False) or _live is not self:
+            raise N.VcrtError("Renderer (closed, or replaced by a later one)",
+                              N.VK_ERROR_INITIALIZATION_FAILED)
+        return self._lib
 
     def __enter__(self):
         return self
@@ -182,19 +207,21 @@ class Renderer:
         self.close()
 
     def close(self):
-        if getattr(self, "_open", False):
+        global _live
+        if getattr(self, "_open", False) and _live is self:
             self._lib.vcrt_end()
-            self._open = False
+            _live = None
+        self._open = False
 
     def set_scene(self, scene) -> None:
         arr = builtin_scene(scene) if isinstance(scene, (str, int)) else scene
         arr = np.ascontiguousarray(arr, dtype=SPHERE_DTYPE)
         self._scene = arr
-        N.check("vcrt_set_scene", self._lib.vcrt_set_scene(
+        N.check("vcrt_set_scene", self._L().vcrt_set_scene(
             arr.ctypes.data_as(ctypes.POINTER(N.vcrt_sphere)), len(arr)))
 
     def draw_next_frame(self) -> None:
-        N.check("vcrt_draw_next_frame", self._lib.vcrt_draw_next_frame())
+        N.check("vcrt_draw_next_frame", self._L().vcrt_draw_next_frame())
 
     def comm_init(self, comm_id: bytes) -> None:
         """Join the multi-GPU frame gather (vcrt_comm_init, RCCL inside libvcrt): every rank
@@ -205,13 +232,13 @@ class Renderer:
             raise ValueError("a comm id is 128 bytes (vcrt_comm_unique_id)")
         cid = N.vcrt_comm_id()
         ctypes.memmove(ctypes.addressof(cid), raw, len(raw))  # c_char arrays stop at NUL
-        N.check("vcrt_comm_init", self._lib.vcrt_comm_init(ctypes.byref(cid)))
+        N.check("vcrt_comm_init", self._L().vcrt_comm_init(ctypes.byref(cid)))
         self._gathering = True
 
     def local_layout(self) -> tuple[int, int]:
         """(float4 elements, tiles) of the rank-local framebuffer."""
         e, t = ctypes.c_uint32(), ctypes.c_uint32()
-        N.check("vcrt_local_layout", self._lib.vcrt_local_layout(ctypes.byref(e), ctypes.byref(t)))
+        N.check("vcrt_local_layout", self._L().vcrt_local_layout(ctypes.byref(e), ctypes.byref(t)))
         return e.value, t.value
 
     def _frame_shape(self) -> tuple[int, ...]:
@@ -227,7 +254,7 @@ class Renderer:
         8*(y%8) + x%8)."""
         shape = self._frame_shape()
         out = np.empty(shape, dtype=np.float32)
-        N.check("vcrt_read_framebuffer", self._lib.vcrt_read_framebuffer(
+        N.check("vcrt_read_framebuffer", self._L().vcrt_read_framebuffer(
             out.ctypes.data_as(ctypes.c_void_p), out.size))
         return out
 
@@ -236,42 +263,42 @@ class Renderer:
         swapchain shows), uint8 with the read_framebuffer shape."""
         shape = self._frame_shape()
         out = np.empty(shape, dtype=np.uint8)
-        N.check("vcrt_read_framebuffer_srgb8", self._lib.vcrt_read_framebuffer_srgb8(
+        N.check("vcrt_read_framebuffer_srgb8", self._L().vcrt_read_framebuffer_srgb8(
             out.ctypes.data_as(ctypes.c_void_p), out.size))
         return out
 
     def reset_accumulation(self) -> None:
-        N.check("vcrt_reset_accumulation", self._lib.vcrt_reset_accumulation())
+        N.check("vcrt_reset_accumulation", self._L().vcrt_reset_accumulation())
 
     def framebuffer_device(self) -> tuple[int, int]:
         p, n = ctypes.c_void_p(), ctypes.c_size_t()
         N.check("vcrt_framebuffer_device",
-                self._lib.vcrt_framebuffer_device(ctypes.byref(p), ctypes.byref(n)))
+                self._L().vcrt_framebuffer_device(ctypes.byref(p), ctypes.byref(n)))
         return p.value or 0, n.value
 
     def set_framebuffer_device(self, ptr: int | None, nbytes: int = 0) -> None:
         N.check("vcrt_set_framebuffer_device",
-                self._lib.vcrt_set_framebuffer_device(ctypes.c_void_p(ptr or None), nbytes))
+                self._L().vcrt_set_framebuffer_device(ctypes.c_void_p(ptr or None), nbytes))
 
     def assemble_tiles(self, gathered_ptr: int, frame_ptr: int, tiles_per_rank: int) -> None:
         d = self.desc
-        N.check("vcrt_assemble_tiles", self._lib.vcrt_assemble_tiles(
+        N.check("vcrt_assemble_tiles", self._L().vcrt_assemble_tiles(
             ctypes.c_void_p(gathered_ptr), ctypes.c_void_p(frame_ptr), d.width, d.height,
             d.world_size, tiles_per_rank))
 
     def shader_load(self, path: str) -> None:
-        N.check("vcrt_shader_load", self._lib.vcrt_shader_load(path.encode()))
+        N.check("vcrt_shader_load", self._L().vcrt_shader_load(path.encode()))
 
     def frame_times(self) -> tuple:
         """(kernel_ms, segments, gather_ms, frame_ms) of the last frame: vcrt_get_stats into a
         reused struct, without building stats()'s dict (a timed loop's per-frame bookkeeping)."""
         s = self._frame_stats
-        N.check("vcrt_get_stats", self._lib.vcrt_get_stats(ctypes.byref(s)))
+        N.check("vcrt_get_stats", self._L().vcrt_get_stats(ctypes.byref(s)))
         return s.kernel_ms, s.segments, s.gather_ms, s.frame_ms
 
     def stats(self) -> dict:
         s = N.vcrt_stats()
-        N.check("vcrt_get_stats", self._lib.vcrt_get_stats(ctypes.byref(s)))
+        N.check("vcrt_get_stats", self._L().vcrt_get_stats(ctypes.byref(s)))
         out = {name: getattr(s, name) for name, _ in N.vcrt_stats._fields_}
         out["debug"] = list(s.debug)
         out["kernel"] = s.kernel.decode()
