@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, W=W, H=H):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -48,9 +48,10 @@ def _worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_reassembles_bitwise(tmp_path, world):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+@pytest.mark.parametrize("world,w,h", [(2, W, H), (3, W, H),
+                                       (3, 8, 8), (4, 9, 9)])  # ranks that own no tile
+def test_gloo_gather_reassembles_bitwise(tmp_path, world, w, h):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), w, h), nprocs=world, join=True)
     frame = np.load(tmp_path / "frame.npy")
     full = np.load(tmp_path / "full.npy")
     assert np.array_equal(frame.view(np.uint32), full.view(np.uint32))
