@@ -76,7 +76,7 @@ enum : uint32_t {
     kBlockRing, kItem, kCam, kCamBig, kCamBigM0, kCamBigM1, kCamBigM2, kCamBigM3, kCamListTrip,
     kCamRootTrip, kShadeCam, kScan, kScanLinear, kMainBig, kMainBigM0, kMainBigM1, kMainBigM2,
     kMainBigM3, kListed, kLevelChunk, kLevelNodes, kDrainTrip, kPassCand, kPassGroup, kPassNode,
-    kPassChunk, kShadeSkyMain, kSqrtFallback, kDivFallback,
+    kPassChunk, kShadeSkyMain, kSqrtFallback, kDivFallback, kSteal,
     kShadeBase0 = 40, kShadeBase1 = 56,  // the shading's regions, per call site (camera phase,
                                          // main-scan sky), at these offsets:
     kShEntry = 0, kShHit, kShNormalDiv, kShSinFallback, kShLamMetal, kShLam, kShMetal, kShGlass,
@@ -1856,6 +1856,7 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
         // inside made the compiler copy ~20 live registers around the loop on every pass).
         bool got = false;
         uint32_t g_lt = 0u, g_chunk = 0u, g_slot = 0u, g_px = 0u, g_py = 0u, g_ent = 0u;
+        int g_s0 = -1, g_s1 = 0;  // a stolen sample range (the drain below), else -1
         uint64_t need_mask = __ballot(need && !done);
         if constexpr (kFlat) {
             // deferred fetches (TraceParams.fetch_min / fetch_wait): while fewer than fetch_min
@@ -2025,6 +2026,56 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             blk_next += min((uint32_t)__popcll(need_mask), avail);
             need_mask = __ballot(need && !done);
         }
+#ifndef VCRT_NO_STEAL
+        // ---- the drain: once every queue is empty, an idle lane takes the later quanta of
+        //      the wave's longest remaining item (the victim keeps the quantum in progress and
+        //      half of the rest). Quanta are summed on their own and added exactly, so any lane
+        //      may trace any whole quantum of a pixel: the same bits, the same segments. ----
+        if (q_drained >= kQueues && (P.flags & kFlagDirect) == 0u) {
+            uint64_t idle = __ballot(done);
+            if (idle != 0u) {
+                const int gm = (int)P.quantum_mask, G = gm + 1;
+                uint32_t rem = 0u;  // whole quanta after the one in progress
+                if (!done && !need) {
+                    const int next = (sample & ~gm) + G;
+                    if (sample_end > next) rem = (uint32_t)((sample_end - next + gm) / G);
+                }
+                while (idle != 0u) {
+                    region(rrow, reg::kSteal);
+                    const uint32_t top = wave_max_small<10>(rem);  // <= kAccumMaxChunks
+                    if (top == 0u) break;
+                    const uint32_t victim = (uint32_t)__builtin_ctzll(__ballot(rem == top));
+                    const uint32_t thief = (uint32_t)__builtin_ctzll(idle);
+                    idle &= idle - 1u;
+                    const uint32_t give = (top + 1u) >> 1;
+                    const int v_sample = __builtin_amdgcn_readlane(sample, victim);
+                    const int v_end = __builtin_amdgcn_readlane(sample_end, victim);
+                    const uint32_t v_q = __builtin_amdgcn_readlane(q, victim);
+                    const uint32_t v_pxy = __builtin_amdgcn_readlane(pxy, victim);
+                    const int cut = (v_sample & ~gm) + G * (int)(1u + top - give);
+                    if (lane == victim) {
+                        sample_end = cut;
+                        rem = top - give;
+                    }
+                    if (lane == thief) {
+                        got = true;
+                        done = false;
+                        need = false;
+                        g_lt = (v_q & kQMask) >> 6;
+                        g_slot = v_q & 63u;
+                        g_ent = v_q >> kRingQBits;
+                        g_px = v_pxy & 0xffffu;
+                        g_py = v_pxy >> 16;
+                        g_s0 = cut;
+                        g_s1 = v_end;
+                        // no victim before its range is set up (the got block below): its
+                        // sample / sample_end / q still name the item it finished
+                        rem = 0u;
+                    }
+                }
+            }
+        }
+#endif
         if constexpr (kStats) pt.items_cur += (uint64_t)__popcll(__ballot(got));
         if (got) {
             region(rrow, reg::kItem);
@@ -2050,6 +2101,12 @@ __device__ __forceinline__ void trace_impl(const TraceParams& p_arg, float4* lds
             const int k = tail ? k_tail : k_head;
             sample = (tail ? t_start : 0) + (int)(g_chunk & 0xffffu) * k;
             sample_end = min(sample + k, tail ? n_spp : t_start);
+#ifndef VCRT_NO_STEAL
+            if (g_s0 >= 0 && g_s0 < g_s1) {  // a stolen range of whole quanta (never empty)
+                sample = g_s0;
+                sample_end = g_s1;
+            }
+#endif
             // first camera ray of the chunk, shader.comp:48-52
             d = camera_dir(sample);
             o = cam;
