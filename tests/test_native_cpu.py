@@ -537,3 +537,29 @@ def test_non_finite_attenuation_makes_nan_pixels_only(oracle):
     nan = np.isnan(img[..., :3]).any(axis=-1)
     assert nan.any() and not nan.all()
     assert np.array_equal(nan, ~np.isfinite(seq[..., :3]).all(axis=-1))
+
+
+def test_drain_steal_split_invariants():
+    """The drain work stealing's arithmetic (tracer.hip, the fetch: `rem`, `give`, `cut`),
+    restated and checked exhaustively on small items: the victim keeps the quantum in progress,
+    the thief's range is non-empty and starts on a quantum boundary, and the two ranges are
+    exactly the victim's remaining samples -- so every quantum is traced once, by one lane."""
+    for G in (1, 2, 4, 8):
+        gm = G - 1
+        for end in range(1, 40):
+            for sample in range(0, end):
+                nxt = (sample & ~gm) + G
+                rem = (end - nxt + gm) // G if end > nxt else 0
+                # rem = the quantum starts in [nxt, end)
+                assert rem == len([s for s in range(nxt, end) if s % G == 0])
+                if rem == 0:
+                    continue
+                give = (rem + 1) >> 1
+                cut = (sample & ~gm) + G * (1 + rem - give)
+                assert sample < cut < end and cut % G == 0
+                victim = set(range(sample, cut))
+                thief = set(range(cut, end))
+                assert victim.isdisjoint(thief) and victim | thief == set(range(sample, end))
+                # the thief's own remaining quanta after its first: give - 1
+                t_next = cut + G
+                assert ((end - t_next + gm) // G if end > t_next else 0) == give - 1
