@@ -324,3 +324,25 @@ def test_a_replaced_renderer_is_stale(oracle):
     want, _ = oracle.render(oracle.config(24, 16, 2, 5, **oracle.partition(st)),
                             oracle.scene("three"))
     assert_bitwise(got, want, "second renderer")
+
+
+def test_progressive_cost_order_across_a_code_object_reload(oracle, monkeypatch):
+    """A progressive renderer on the cost order (forced), whose code object is reloaded between
+    frames: the reload re-keys the block order, so the next frame measures again while it adds
+    to the same sums -- three frames equal the oracle's 3 x spp image, bit for bit."""
+    monkeypatch.setenv("VCRT_WORK_ORDER", "cost")
+    w, h, spp, depth = 72, 40, 6, 12
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0,
+                         progressive=True)
+    with vc.Renderer(desc, "final") as r:
+        k = oracle.partition(r.stats())
+        r.draw_next_frame()
+        r.draw_next_frame()
+        assert r.stats()["cost_order"] == 1
+        r.shader_load(N.CODE_OBJECT_PATH)
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    assert st["accumulated_spp"] == 3 * spp
+    want, _ = oracle.render(oracle.config(w, h, 3 * spp, depth, **k, frame_spp=spp),
+                            oracle.scene("final"))
+    assert_bitwise(got, want, "3 progressive frames around a reload")
