@@ -1,9 +1,10 @@
-"""Diagnostic (test infrastructure: it checks against the oracle): where a large frame departs from the oracle. Renders W x H once per setting
+"""Diagnostic (test infrastructure: the oracle is its checker): where a large frame departs
+from the oracle. Renders W x H once per setting
 (--settings: env assignments per run, e.g. "none" "VCRT_PRIMARY_LISTS=0" "VCRT_ACCUM_RING=0")
 and compares every --step-th row with the oracle's pixels, printing the rows that differ, the
 first of them and a few pixels of it.
 
-  python tools/diag_big_frame.py --width 8192 --height 8192 --spp 8 --depth 3 --step 256
+  python tests/diag_big_frame.py --width 8192 --height 8192 --spp 8 --depth 3 --step 256
 """
 import argparse
 import os
