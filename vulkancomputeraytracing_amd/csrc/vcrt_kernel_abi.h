@@ -87,8 +87,9 @@ struct TraceParams {
     // to the pixel's sums at every sample index that is a multiple of G (vcrt_math.h
     // "Accumulation"); items hold whole quanta
     uint32_t quantum_mask;
-    uint32_t flags;        // kFlag*; bits 24..31: s + 128, the quantization scale 2^s of the
-                           //   quantum sums (vcrt_math.h "Accumulation": per scene), kept in
+    uint32_t flags;        // kFlag*; bits 24..31: s + 128, the quantization scale 2^s every
+                           //   pixel's quantum sums start at (vcrt_math.h "Accumulation":
+                           //   2^32; kFlagPixelScale: each pixel's own from pixel_emax), kept in
                            //   the flags word the retire reads anyway (no load of its own)
     float spp_total;       // kFlagDirect: the divisor (samples per pixel)
     float cam[12];         // pixel00.xyz, delta_u.xyz, delta_v.xyz, center.xyz
