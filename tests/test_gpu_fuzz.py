@@ -346,3 +346,29 @@ def test_progressive_cost_order_across_a_code_object_reload(oracle, monkeypatch)
     want, _ = oracle.render(oracle.config(w, h, 3 * spp, depth, **k, frame_spp=spp),
                             oracle.scene("final"))
     assert_bitwise(got, want, "3 progressive frames around a reload")
+
+
+def test_srgb8_encode_edge_values_bitwise(oracle):
+    """vcrt_encode_srgb8 on every kind of float the framebuffer can hold, through an external
+    device framebuffer: each of the 255 thresholds and its neighbouring floats, values below 0 and
+    above 1, -0, denormals, +-inf and NaN -- against the oracle's encoder byte for byte."""
+    import torch
+    th = np.zeros(255, dtype=np.float32)
+    N.lib().vcrt_srgb8_thresholds(th.ctypes.data)
+    vals = [th, np.nextafter(th, np.float32(-1)), np.nextafter(th, np.float32(2)),
+            np.float32([0.0, -0.0, 1.0, 1e-45, -1e-45, 1e-38, -1.0, 2.0, 1e30, -1e30,
+                        np.inf, -np.inf, np.nan]),
+            np.random.default_rng(3).uniform(-0.5, 1.5, 4096).astype(np.float32)]
+    v = np.concatenate(vals).astype(np.float32)
+    w = 64
+    h = (len(v) + 4 * w - 1) // (4 * w)
+    flat = np.ones(w * h * 4, dtype=np.float32)
+    flat[:len(v)] = v
+    img = flat.reshape(h, w, 4)
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=1, max_depth=1, device=0)
+    buf = torch.from_numpy(img.copy()).to("cuda:0")
+    with vc.Renderer(desc, "red") as r:
+        r.set_framebuffer_device(buf.data_ptr(), buf.numel() * 4)
+        torch.cuda.synchronize()
+        got = r.read_framebuffer_srgb8()
+    assert np.array_equal(got, oracle.encode_srgb8(img))
