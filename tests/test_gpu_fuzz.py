@@ -8,6 +8,8 @@ must give the oracle's bits for every pixel it renders, and its segment count on
 reference loop these restate is shader.comp:42-57 over functions.glsl:65-92; the cases only
 widen the inputs the fixed-configuration tests (test_gpu_parity.py) cover.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -372,3 +374,52 @@ def test_srgb8_encode_edge_values_bitwise(oracle):
         torch.cuda.synchronize()
         got = r.read_framebuffer_srgb8()
     assert np.array_equal(got, oracle.encode_srgb8(img))
+
+
+def _read_ppm(path):
+    with open(path, "rb") as f:
+        data = f.read()
+    parts = data.split(b"\n", 3)
+    assert parts[0] == b"P6" and parts[2] == b"255"
+    w, h = (int(v) for v in parts[1].split())
+    return np.frombuffer(parts[3], dtype=np.uint8, count=w * h * 3).reshape(h, w, 3)
+
+
+@pytest.mark.parametrize("scene,w,h,spp,depth,frames,progressive,fmt", [
+    ("three", 97, 41, 6, 9, 2, 1, "ppm"),
+    ("final", 64, 36, 12, 10, 3, 1, "pfm"),
+    ("red", 33, 70, 3, 4, 2, 0, "ppm"),
+    ("stress4096", 48, 27, 2, 20, 1, 0, "pfm"),
+])
+def test_cpp_host_api_configurations(oracle, tmp_path, scene, w, h, spp, depth, frames,
+                                     progressive, fmt):
+    """bin/vcrt_render (the C++ Begin / Draw / End of Renderer.hpp:14-20 with
+    SetRenderDescription / SetRenderScene) on several scenes, sizes and progressive frame counts,
+    writing PFM (linear) or PPM (sRGB8 encoded on the GPU): the files equal the oracle's image
+    (progressive: frames x spp samples) and its sRGB8 encoding."""
+    import subprocess
+    from tests.test_gpu_configs import read_pfm
+    out = tmp_path / f"frame.{fmt}"
+    cmd = [os.path.join(N.BIN_DIR, "vcrt_render"), "--scene", scene, "--width", str(w),
+           "--height", str(h), "--spp", str(spp), "--depth", str(depth), "--frames",
+           str(frames), "--progressive", str(progressive), "--out", str(out)]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    q = vc.renderer.work_quantum(vc.RenderDesc(width=w, height=h, samples_per_pixel=spp,
+                                               max_depth=depth, progressive=bool(progressive)))
+    total = spp * (frames if progressive else 1)
+    want, _ = oracle.render(oracle.config(w, h, total, depth, quantum=q,
+                                          frame_spp=spp if progressive else 0),
+                            oracle.scene(scene))
+    if fmt == "pfm":
+        assert_bitwise(read_pfm(out), want[..., :3], f"{scene} pfm")
+    else:
+        assert np.array_equal(_read_ppm(out), oracle.encode_srgb8(want)[..., :3])
+
+
+def test_cpp_host_api_unwritable_output_fails(tmp_path):
+    import subprocess
+    res = subprocess.run([os.path.join(N.BIN_DIR, "vcrt_render"), "--scene", "red", "--width",
+                          "16", "--height", "16", "--out", str(tmp_path / "no" / "x.ppm")],
+                         capture_output=True, text=True, timeout=120)
+    assert res.returncode == 1 and "cannot write" in res.stderr

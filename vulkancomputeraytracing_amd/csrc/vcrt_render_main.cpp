@@ -2,6 +2,7 @@
 // (VulkanComputeRayTracing.cpp:17-42): Begin -> DrawNextFrame x N -> End, then optionally writes
 // the frame as PFM (linear rgba32f, as the compute image holds it) or PPM (sRGB8 encoded on the
 // GPU, as the B8G8R8A8_SRGB swapchain shows it: Frontend.cpp:43).
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -93,6 +94,10 @@ int main(int argc, char** argv) {
                 }
             }
             std::fclose(f);
+        } else {
+            std::fprintf(stderr, "cannot write %s: %s\n", out.c_str(),
+                         r == VK_SUCCESS ? std::strerror(errno) : vcrt_result_string(r));
+            if (r == VK_SUCCESS) r = VK_ERROR_UNKNOWN;
         }
     }
     EndRenderingOperation();
