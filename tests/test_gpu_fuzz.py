@@ -423,3 +423,23 @@ def test_cpp_host_api_unwritable_output_fails(tmp_path):
                           "16", "--height", "16", "--out", str(tmp_path / "no" / "x.ppm")],
                          capture_output=True, text=True, timeout=120)
     assert res.returncode == 1 and "cannot write" in res.stderr
+
+
+@pytest.mark.parametrize("fetch", [None, ("1", "0"), ("16", "4")])
+def test_deferred_fetch_keeps_bits(oracle, monkeypatch, fetch):
+    """The flat scan's deferred fetch (the LDS-table scan waits for 4 lanes by default) only
+    changes when lanes start their items: the default, immediate fetches and long deferrals give
+    the oracle's bits and segment counts."""
+    if fetch is not None:
+        monkeypatch.setenv("VCRT_FETCH_MIN", fetch[0])
+        monkeypatch.setenv("VCRT_FETCH_WAIT", fetch[1])
+    w, h, spp, depth = 160, 90, 16, 10
+    desc = vc.RenderDesc(width=w, height=h, samples_per_pixel=spp, max_depth=depth, device=0)
+    with vc.Renderer(desc, "final") as r:
+        r.draw_next_frame()
+        got, st = r.read_framebuffer(), r.stats()
+    assert st["kernel"].startswith("vcrt_trace_cull_flat")
+    want, segs = oracle.render(oracle.config(w, h, spp, depth, **oracle.partition(st)),
+                               oracle.scene("final"))
+    assert_bitwise(got, want, f"fetch {fetch}")
+    assert st["segments"] == segs

@@ -81,8 +81,9 @@ struct RendererState {
     size_t cost_words = 0, order_words = 0;
     uint64_t order_key = 0;  // the configuration the order was measured for (0: none)
     uint32_t nch_magic[2] = {0u, 0u};  // TraceParams.nch_magic of the partition
-    // deferred fetches (TraceParams.fetch_min / fetch_wait; VCRT_FETCH_MIN, VCRT_FETCH_WAIT)
-    uint32_t fetch_min = 1u, fetch_wait = 0u;
+    // deferred fetches (TraceParams.fetch_min / fetch_wait; VCRT_FETCH_MIN, VCRT_FETCH_WAIT;
+    // fetch_min 0: the rule in trace_frame)
+    uint32_t fetch_min = 0u, fetch_wait = 0u;
     int flat_block = 0;  // VCRT_FLAT_BLOCK: threads per group of the LDS flat scan (0: 256)
     uint32_t lds_per_cu = 0;     // LDS bytes per CU (160 KB on gfx950)
     // diagnostics (environment: VCRT_DEBUG_STATS=1, VCRT_WORK_ORDER=forward)
@@ -1369,8 +1370,6 @@ static VkResult trace_frame(uint64_t spp_total, uint32_t* outlier_max) {
         return VK_ERROR_INITIALIZATION_FAILED;
     p.spp_total = static_cast<float>(spp_total);
     p.region = nullptr;
-    p.fetch_min = g.fetch_min;
-    p.fetch_wait = g.fetch_wait;
     p.nch_magic[0] = g.nch_magic[0];
     p.nch_magic[1] = g.nch_magic[1];
     for (int j = 0; j < 13; j++) p.sin_c[j] = vcrt::kSinC[j];
@@ -1378,6 +1377,13 @@ static VkResult trace_frame(uint64_t spp_total, uint32_t* outlier_max) {
     for (int i = 0; i < 12; i++) p.cam[i] = cam[i];
     const KernelChoice kc = select_kernel();
     hipFunction_t f = g.debug_stats == 1 ? kc.stats : kc.f;
+    // Deferred fetches (tracer.hip, the flat scans): the LDS-table flat scan waits until 4 lanes
+    // need an item (at most one iteration): C3 -0.6 % kernel time (its 16 items per pixel make
+    // the fetch frequent), C4 and the 8-way shards within 0.1 %, same bits; the global-table and
+    // boxes-in-LDS scans fetch at once (C5 +0.6 % with it). profiles/r06_ab_log.md.
+    const bool lds_flat = kc.f == g.k_trace_cull_flat;
+    p.fetch_min = g.fetch_min > 0u ? g.fetch_min : (lds_flat ? 4u : 1u);
+    p.fetch_wait = g.fetch_min > 0u ? g.fetch_wait : (lds_flat ? 1u : 0u);
     const uint32_t block = kc.block;
     uint32_t lds = kc.lds;
     // the linear SMEM scan of a small scene stages its shading and jitter tables in LDS
